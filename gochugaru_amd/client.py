@@ -1,0 +1,197 @@
+"""Client façade — host-side mirror of gochugaru's check family, answered locally.
+
+Mirrors ``client/client.go``:
+
+* ``Check``      (``:238-284``)  — items in request order; HAS_PERMISSION -> True, NO and
+  CONDITIONAL -> False (``:274-277``); the first per-item error returns the results so far
+  plus the error (``:279-280``); an empty request returns ``[]`` (``client_test.go:203-207``).
+* ``CheckOne``   (``:129-135``), ``CheckAny`` (``:138-145``), ``CheckAll`` (``:148-160``),
+  ``CheckIter``  (``:164-180``, chunks of 1000 by default, stops at the first error).
+* ``checkOverlap`` (``:182-191``) — raises (Go panics) when ``WithOverlapRequired`` is set and
+  the context carries no overlap key.
+* ``retryRetriableErrors`` (``:193-211``) — exponential backoff 50 ms -> 2 s on Unavailable
+  (``GCK_E_DEVICE``, ``GCK_E_REVISION``) and DeadlineExceeded; anything else is permanent.
+
+The round-trip to SpiceDB (``:261-266``) is replaced by ``Engine.check_bulk`` on the GPU.
+Go's ``(results, err)`` return pairs are kept as Python tuples so that callers and tests read
+like the reference.
+"""
+from __future__ import annotations
+
+import random
+import time
+from typing import Iterable, Iterator, List, Optional, Tuple
+
+from . import consistency as _cs
+from .consistency import Background, Context, Strategy
+from .engine import (CONSISTENCY_AT_LEAST, CONSISTENCY_FULL, CONSISTENCY_MIN_LATENCY,
+                     CONSISTENCY_SNAPSHOT, GCK_E_DEVICE, GCK_E_REVISION, ITEM_ERROR_MESSAGES,
+                     PERM_HAS, Engine, GckError)
+
+CHECK_ITER_CHUNK = 1000  # client/client.go:166
+
+
+class OverlapKeyPanic(RuntimeError):
+    """Go panics in checkOverlap (client/client.go:190)."""
+
+
+class CheckItemError(Exception):
+    """A CheckBulkPermissionsPair_Error turned into a Go error (client/client.go:279-280)."""
+
+
+class Unavailable(Exception):
+    pass
+
+
+class InvalidArgument(Exception):
+    pass
+
+
+def WithOverlapRequired():
+    """``client/client.go:84-86``."""
+    def opt(c: "Client"):
+        c.overlapRequired = True
+    return opt
+
+
+def _requirement(cs: Optional[Strategy]) -> Tuple[int, int]:
+    if cs is None:
+        return CONSISTENCY_MIN_LATENCY, 0
+    v = cs.V1Consistency
+    if v.requirement == _cs.MINIMIZE_LATENCY:
+        return CONSISTENCY_MIN_LATENCY, 0
+    if v.requirement == _cs.FULLY_CONSISTENT:
+        return CONSISTENCY_FULL, 0
+    try:
+        rev = int(v.token)
+    except (TypeError, ValueError):
+        raise InvalidArgument(f"invalid zedtoken {v.token!r}")
+    if v.requirement == _cs.AT_LEAST_AS_FRESH:
+        return CONSISTENCY_AT_LEAST, rev
+    if v.requirement == _cs.AT_EXACT_SNAPSHOT:
+        return CONSISTENCY_SNAPSHOT, rev
+    raise InvalidArgument(f"unknown consistency requirement {v.requirement!r}")
+
+
+def _retriable(err: BaseException) -> bool:
+    if isinstance(err, GckError):
+        return err.code in (GCK_E_DEVICE, GCK_E_REVISION)  # gRPC Unavailable
+    msg = str(err)
+    return isinstance(err, (Unavailable, TimeoutError)) or \
+        "retryable error" in msg or "try restarting transaction" in msg
+
+
+def retryRetriableErrors(ctx: Context, fn, max_elapsed: float = 15 * 60):
+    """``client/client.go:193-211``: backoff.ExponentialBackOff{Initial 50ms, Max 2s,
+    default multiplier 1.5 and randomization 0.5}; gives up at the context deadline (or the
+    backoff's default 15 min max elapsed time)."""
+    interval = 0.05
+    start = time.monotonic()
+    deadline = getattr(ctx, "deadline", None)
+    while True:
+        try:
+            return fn()
+        except Exception as err:  # noqa: BLE001 — classified below
+            if not _retriable(err):
+                raise
+            delay = interval * (1 + random.uniform(-0.5, 0.5))
+            now = time.monotonic()
+            limit = start + max_elapsed if deadline is None else deadline
+            if now + delay > limit:
+                raise
+            time.sleep(delay)
+            interval = min(interval * 1.5, 2.0)
+
+
+class Client:
+    """``client.Client`` (``client/client.go:101-105``) with a local GPU evaluator in place of
+    the gRPC connection."""
+
+    def __init__(self, engine: Engine, *opts, chunk: int = 65536):
+        self.engine = engine
+        self.overlapRequired = False
+        self.chunk = chunk
+        for o in opts:
+            o(self)
+
+    @classmethod
+    def NewWithOpts(cls, engine: Engine, *opts) -> Tuple["Client", Optional[Exception]]:
+        """``client/client.go:65-75``."""
+        return cls(engine, *opts), None
+
+    # ---- overlap guard -------------------------------------------------------------------
+    def checkOverlap(self, ctx: Optional[Context]):
+        if self.overlapRequired:
+            md = (ctx or Background).metadata
+            if md.get(_cs.REQUEST_OVERLAP_KEY):
+                return
+            raise OverlapKeyPanic("failed to configure required overlap key for request")
+
+    # ---- the check family ----------------------------------------------------------------
+    def Check(self, ctx: Optional[Context], cs: Optional[Strategy], *rs) -> Tuple[List[bool], Optional[Exception]]:
+        self.checkOverlap(ctx)
+        rels = [r.Relationship() for r in rs]
+        try:
+            requirement, revision = _requirement(cs)
+            items = self.engine.make_items(rels)
+            perm, err = retryRetriableErrors(
+                ctx or Background,
+                lambda: self.engine.check_bulk(items, requirement, revision))
+        except Exception as e:  # noqa: BLE001 — Go returns (nil, err)
+            return None, e
+        results: List[bool] = []
+        for p, e in zip(perm.tolist(), err.tolist()):
+            if e:
+                return results, CheckItemError(ITEM_ERROR_MESSAGES.get(e, f"item error {e}"))
+            results.append(p == PERM_HAS)
+        return results, None
+
+    def CheckOne(self, ctx, cs, r) -> Tuple[bool, Optional[Exception]]:
+        results, err = self.Check(ctx, cs, r)
+        if err is not None:
+            return False, err
+        return results[0], None
+
+    def CheckAny(self, ctx, cs, *rs) -> Tuple[bool, Optional[Exception]]:
+        results, err = self.Check(ctx, cs, *rs)
+        if err is not None:
+            return False, err
+        return True in results, None
+
+    def CheckAll(self, ctx, cs, *rs) -> Tuple[bool, Optional[Exception]]:
+        results, err = self.Check(ctx, cs, *rs)
+        if err is not None:
+            return False, err
+        for r in results:
+            if not r:
+                return False, None
+        return True, None
+
+    def CheckIter(self, ctx, cs, rs: Iterable, chunk: int = CHECK_ITER_CHUNK) -> Iterator[Tuple[bool, Optional[Exception]]]:
+        buf = []
+        for r in rs:
+            buf.append(r)
+            if len(buf) == chunk:
+                ok = yield from self._iter_chunk(ctx, cs, buf)
+                if not ok:
+                    return
+                buf = []
+        if buf:
+            yield from self._iter_chunk(ctx, cs, buf)
+
+    def _iter_chunk(self, ctx, cs, items):
+        checks, err = self.Check(ctx, cs, *items)
+        if err is not None:
+            yield False, err
+            return False
+        for c in checks:
+            yield c, None
+        return True
+
+    # ---- snapshot plumbing (ReadSchema + ExportRelationships at its revision) -------------
+    def LoadSnapshot(self, schema: str, revision: int, relationships: Iterable) -> None:
+        """Ingest the output of ``ReadSchema`` (client/client.go:416-422) and
+        ``ExportRelationships`` at that revision (client/client.go:472-499)."""
+        self.engine.load_schema(schema)
+        lines = "\n".join(r.String() if hasattr(r, "String") else str(r) for r in relationships)
+        self.engine.load_snapshot_text(revision, lines)

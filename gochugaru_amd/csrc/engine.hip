@@ -1,0 +1,954 @@
+// engine.hip — MI355X (gfx950) batched permission-check kernels and batch driver.
+//
+// Replaces SpiceDB's CheckBulkPermissions dispatch (the computation behind
+// client/client.go:261-266; semantics SURVEY.md §5.1) with a level-synchronous, multi-query
+// frontier expansion over HBM-resident CSR tuple tables:
+//
+//   level L frontier: Entry{query, object, node, depth, cond}
+//     k_expand  : one lane per entry — identity filter, depth budget, direct-subject
+//                 membership (binary search over the sorted CSR row, wildcard = last id),
+//                 computed usersets pushed directly, userset/arrow rows emitted as segments,
+//                 intersection/exclusion/all() nodes spawn a join of sub-queries
+//     k_edges   : one lane per enumerated edge (load-balanced over the segments) — pushes
+//                 the neighbour's (query, object, node) into the next frontier after a
+//                 visited-hash dedupe (memoised per query, SURVEY §8d counting rule)
+//     k_resolve : one lane per query — a query with a Y is decided; a query with no live
+//                 entries and no pending joins is decided N/C/ERR; decisions cascade into
+//                 joins (tri-state algebra) and up to the parent query
+//   level L+1 ...
+//
+// Every frontier level is one dispatch wave of SpiceDB's recursion, so the depth budget
+// (max_depth, default 50) is enforced per entry exactly as dispatch.CheckDepth does.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+
+#include "engine.hpp"
+
+namespace gck {
+
+#define HIP_OK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t err_ = (x);                                                                \
+    if (err_ != hipSuccess)                                                               \
+      throw Error(GCK_E_DEVICE, std::string(#x " failed: ") + hipGetErrorString(err_));   \
+  } while (0)
+
+constexpr int kBlock = 256;
+constexpr unsigned long long kEmptyKey = ~0ull;
+constexpr uint32_t kResErr = 0xF;
+
+struct DeviceSnapshot {
+  std::vector<void*> allocs;
+  DevNode* nodes = nullptr;
+  DevItem* items = nullptr;
+  DevCSR* csrs = nullptr;
+  uint32_t* type_counts = nullptr;
+  uint32_t n_nodes = 0, n_items = 0, n_csrs = 0, n_types = 0, n_rels = 0;
+  uint32_t node_bits = 1, q_bits = 1;
+  uint64_t bytes = 0;
+};
+
+struct Workspace {
+  size_t max_batch = 0, frontier_cap = 0, seg_cap = 0, query_cap = 0, join_cap = 0;
+  uint64_t visited_cap = 0;
+  DevCheck* checks = nullptr;
+  int32_t* item_err = nullptr;
+  DevQuery* queries = nullptr;
+  DevJoin* joins = nullptr;
+  Entry* fr[2] = {nullptr, nullptr};
+  Segment* segs = nullptr;
+  unsigned long long* visited = nullptr;
+  DevCounters* ctr = nullptr;
+  DevCounters* h_ctr = nullptr;  // pinned
+  gck_item* d_items = nullptr;   // staging for the host-buffer API
+  uint8_t* d_perm = nullptr;
+  int32_t* d_err = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  std::vector<void*> allocs;
+};
+
+// ---- device helpers --------------------------------------------------------------------------
+
+struct Ctx {
+  const DevNode* nodes;
+  const DevItem* items;
+  const DevCSR* csrs;
+  const uint32_t* type_counts;
+  uint32_t n_types, n_rels;
+  DevCheck* checks;
+  DevQuery* queries;
+  DevJoin* joins;
+  Entry* next;
+  Segment* segs;
+  unsigned long long* visited;
+  uint64_t vmask;
+  DevCounters* ctr;
+  uint32_t frontier_cap, seg_cap, query_cap, join_cap;
+  uint32_t node_shift, q_shift;  // key = q << q_shift | node << node_shift | cond << 32 | obj
+  uint32_t level, max_depth;
+  int64_t now_us;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ unsigned long long make_key(const Ctx& c, uint32_t q, uint32_t node,
+                                                       uint32_t cond, uint32_t obj) {
+  return ((unsigned long long)q << c.q_shift) | ((unsigned long long)node << c.node_shift) |
+         ((unsigned long long)(cond & 1u) << 32) | obj;
+}
+
+__device__ __forceinline__ bool vlookup(const Ctx& c, unsigned long long key) {
+  uint64_t h = mix64(key) & c.vmask;
+  for (int p = 0; p < 64; ++p) {
+    unsigned long long v = __hip_atomic_load(&c.visited[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == key) return true;
+    if (v == kEmptyKey) return false;
+    h = (h + 1) & c.vmask;
+  }
+  return false;
+}
+
+// 1 = inserted, 0 = already present, -1 = table overflow
+__device__ __forceinline__ int vinsert(const Ctx& c, unsigned long long key) {
+  uint64_t h = mix64(key) & c.vmask;
+  for (int p = 0; p < 128; ++p) {
+    unsigned long long v = __hip_atomic_load(&c.visited[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == key) return 0;
+    if (v == kEmptyKey) {
+      unsigned long long prev = atomicCAS(&c.visited[h], kEmptyKey, key);
+      if (prev == kEmptyKey) return 1;
+      if (prev == key) return 0;
+    }
+    h = (h + 1) & c.vmask;
+  }
+  atomicOr(&c.ctr->overflow, 1u);
+  return -1;
+}
+
+__device__ __forceinline__ uint32_t qflags(const DevQuery* q) {
+  return __hip_atomic_load(&q->flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void set_found(const Ctx& c, uint32_t q, uint32_t cond) {
+  atomicOr(&c.queries[q].flags, cond ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
+}
+
+__device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node,
+                                           uint32_t depth, uint32_t cond) {
+  if (cond && vlookup(c, make_key(c, q, node, 0, obj))) return;  // unconditional visit exists
+  if (vinsert(c, make_key(c, q, node, cond, obj)) <= 0) return;
+  unsigned idx = atomicAdd(&c.ctr->next_size, 1u);
+  if (idx >= c.frontier_cap) {
+    atomicOr(&c.ctr->overflow, 2u);
+    return;
+  }
+  Entry e;
+  e.q = q;
+  e.obj = obj;
+  e.node = node;
+  e.depth = (uint8_t)(depth > 255 ? 255 : depth);
+  e.cond = (uint8_t)cond;
+  c.next[idx] = e;
+  c.queries[q].last_alive = c.level + 1;  // benign race: every writer stores the same value
+}
+
+// lower_bound of `sid` in the CSR row of `obj`; returns the position or kNone.
+__device__ __forceinline__ uint32_t row_find(const DevCSR& r, uint32_t obj, uint32_t sid,
+                                             uint32_t& probes) {
+  if (obj >= r.n_rows) return kNone;
+  uint32_t lo = r.off[obj], hi = r.off[obj + 1];
+  const uint32_t end = hi;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    ++probes;
+    if (r.nbr[mid] < sid) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < end) {
+    if (hi == end) ++probes;  // the final equality read when the loop never touched lo
+    if (r.nbr[lo] == sid) return lo;
+  }
+  return kNone;
+}
+
+__device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t now_us) {
+  if (!r.is_ext) return true;
+  int64_t x = r.exp_us[pos];
+  return x == 0 || x > now_us;
+}
+
+__device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_t obj, uint32_t q,
+                                             uint16_t target, uint32_t depth, uint32_t cond,
+                                             uint32_t& rows) {
+  if (csr == kNone || target == kNoNode) return;
+  const DevCSR& r = c.csrs[csr];
+  if (obj >= r.n_rows) return;
+  ++rows;
+  uint32_t b = r.off[obj], e = r.off[obj + 1];
+  if (e == b) return;
+  unsigned long long packed =
+      atomicAdd(&c.ctr->seg_ctr, (1ull << 40) | (unsigned long long)(e - b));
+  uint32_t si = (uint32_t)(packed >> 40);
+  if (si >= c.seg_cap) {
+    atomicOr(&c.ctr->overflow, 4u);
+    return;
+  }
+  Segment s;
+  s.edge_start = packed & ((1ull << 40) - 1);
+  s.q = q;
+  s.begin = b;
+  s.len = e - b;
+  s.csr = csr;
+  s.target = target;
+  s.depth = (uint8_t)(depth > 255 ? 255 : depth);
+  s.cond = (uint8_t)cond;
+  s.pad = 0;
+  c.segs[si] = s;
+}
+
+// Spawn a join (intersection / exclusion / all-arrow) for node `node` at `obj` on behalf of
+// query `q`. Each operand becomes a child query with its own memoised frontier.
+__device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth,
+                           uint32_t cond, uint32_t& rows) {
+  const DevNode nd = c.nodes[node];
+  uint32_t n_ops = 0;
+  if (nd.kind == NK_ARROW_ALL) {
+    bool missing = false;
+    for (uint32_t k = 0; k < nd.count; ++k) {
+      const DevItem it = c.items[nd.first + k];
+      for (int pass = 0; pass < 2; ++pass) {
+        uint32_t ci = pass ? it.csr_ext : it.csr_plain;
+        if (ci == kNone) continue;
+        const DevCSR& r = c.csrs[ci];
+        if (obj >= r.n_rows) continue;
+        ++rows;
+        uint32_t b = r.off[obj], e = r.off[obj + 1];
+        for (uint32_t p = b; p < e; ++p) {
+          if (!visible(r, p, c.now_us)) continue;
+          if (it.target == kNoNode) missing = true;
+          ++n_ops;
+        }
+      }
+    }
+    if (n_ops == 0 || missing) return;  // all() over nothing, or a subject lacking the target: NO
+  } else if (nd.kind == NK_NIL) {
+    return;
+  } else {
+    n_ops = nd.count;
+  }
+  unsigned j = atomicAdd(&c.ctr->n_joins, 1u);
+  unsigned q0 = atomicAdd(&c.ctr->n_queries, n_ops);
+  if (j >= c.join_cap) {
+    atomicOr(&c.ctr->overflow, 16u);
+    return;
+  }
+  if (q0 + n_ops > c.query_cap) {
+    atomicOr(&c.ctr->overflow, 8u);
+    return;
+  }
+  DevJoin J;
+  J.parent_q = q;
+  J.first_child = q0;
+  J.n_ops = n_ops;
+  J.op = nd.kind;
+  J.cond = cond;
+  J.remaining = (int32_t)n_ops;
+  J.state = 0;
+  J.pad = 0;
+  c.joins[j] = J;
+  const uint32_t check = c.queries[q].check;
+  for (uint32_t k = 0; k < n_ops; ++k) {
+    DevQuery cq;
+    cq.check = check;
+    cq.parent_join = j;
+    cq.flags = 0;
+    cq.pending_joins = 0;
+    cq.last_alive = c.level;  // raised to level+1 by push_entry
+    cq.operand = k;
+    c.queries[q0 + k] = cq;
+  }
+  __hip_atomic_fetch_add(&c.queries[q].pending_joins, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (nd.kind == NK_ARROW_ALL) {
+    uint32_t k = 0;
+    for (uint32_t t = 0; t < nd.count; ++t) {
+      const DevItem it = c.items[nd.first + t];
+      for (int pass = 0; pass < 2; ++pass) {
+        uint32_t ci = pass ? it.csr_ext : it.csr_plain;
+        if (ci == kNone) continue;
+        const DevCSR& r = c.csrs[ci];
+        if (obj >= r.n_rows) continue;
+        uint32_t b = r.off[obj], e = r.off[obj + 1];
+        for (uint32_t p = b; p < e; ++p) {
+          if (!visible(r, p, c.now_us)) continue;
+          uint32_t cav = r.is_ext ? (r.cav[p] != 0) : 0u;
+          push_entry(c, q0 + k, r.nbr[p], it.target, depth + 1, cav);
+          ++k;
+        }
+      }
+    }
+  } else {
+    for (uint32_t k = 0; k < n_ops; ++k) {
+      const DevItem it = c.items[nd.first + k];
+      push_entry(c, q0 + k, obj, it.target, depth + it.dispatch, 0u);
+    }
+  }
+}
+
+// ---- kernels -----------------------------------------------------------------------------
+
+__device__ __forceinline__ void wave_add(unsigned long long* p, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, v);
+}
+
+__global__ void __launch_bounds__(kBlock) k_init(Ctx c, const gck_item* __restrict__ items,
+                                                 uint32_t n, Entry* __restrict__ fr0,
+                                                 int32_t* __restrict__ item_err) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gck_item it = items[i];
+  int32_t err = GCK_ITEM_OK;
+  if (it.resource_type >= c.n_types || it.subject_type >= c.n_types) {
+    err = GCK_ITEM_ERR_UNKNOWN_TYPE;
+  } else if (it.permission >= c.n_rels || c.nodes[it.permission].type != it.resource_type) {
+    err = GCK_ITEM_ERR_UNKNOWN_PERMISSION;
+  } else if (it.subject_relation != kEllipsis &&
+             (it.subject_relation >= c.n_rels ||
+              c.nodes[it.subject_relation].type != it.subject_type)) {
+    err = GCK_ITEM_ERR_UNKNOWN_SUBJECT_RELATION;
+  } else if (it.subject_id == kWildcard) {
+    err = GCK_ITEM_ERR_WILDCARD_SUBJECT;
+  }
+  item_err[i] = err;
+  DevCheck ck;
+  ck.sid = it.subject_id;
+  ck.stype = it.subject_type;
+  ck.srel = it.subject_relation;
+  c.checks[i] = ck;
+  DevQuery q;
+  q.check = i;
+  q.parent_join = kNone;
+  q.pending_joins = 0;
+  q.last_alive = 0;
+  q.operand = 0;
+  q.flags = 0;
+  if (err != GCK_ITEM_OK) {
+    q.flags = QF_DONE | (kResErr << QF_RES_SHIFT);
+  } else if (it.resource_id >= c.type_counts[it.resource_type]) {
+    // unknown object: no relationships (client/client_test.go:209-215) unless it is the
+    // subject itself (identity filter)
+    bool ident = it.resource_type == it.subject_type && it.permission == it.subject_relation &&
+                 it.resource_id == it.subject_id && it.resource_id != kAbsent;
+    q.flags = QF_DONE | ((ident ? GCK_PERM_HAS : GCK_PERM_NO) << QF_RES_SHIFT);
+  }
+  c.queries[i] = q;
+  Entry e;
+  e.q = i;
+  e.obj = it.resource_id;
+  e.node = it.permission;
+  e.depth = 0;
+  e.cond = 0;
+  fr0[i] = e;
+}
+
+__global__ void __launch_bounds__(kBlock) k_expand(Ctx c, const Entry* __restrict__ cur, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t rows = 0, probes = 0, expanded = 0;
+  if (i < n) {
+    const Entry e = cur[i];
+    DevQuery* q = &c.queries[e.q];
+    uint32_t qf = qflags(q);
+    if (!(qf & QF_DONE)) {
+      ++expanded;
+      const DevCheck s = c.checks[q->check];
+      const DevNode nd = c.nodes[e.node];
+      bool done = false;
+      if ((nd.flags & NF_REAL) && e.node == s.srel && nd.type == s.stype && e.obj == s.sid) {
+        set_found(c, e.q, e.cond);  // filterForFoundMemberResource
+        done = true;
+      } else if (e.depth >= c.max_depth) {
+        atomicOr(&q->flags, (uint32_t)QF_ERR);  // dispatch.CheckDepth: max depth exceeded
+        done = true;
+      }
+      if (!done) {
+        switch (nd.kind) {
+          case NK_RELATION: {
+            // pass 1: direct subject + wildcard membership (checkDirect)
+            for (uint32_t k = 0; k < nd.count && !done; ++k) {
+              const DevItem it = c.items[nd.first + k];
+              if (it.stype != s.stype) continue;
+              const bool direct = it.srel == s.srel;
+              const bool wild = it.srel == kEllipsis && s.srel == kEllipsis;
+              if (!direct && !wild) continue;
+              for (int pass = 0; pass < 2 && !done; ++pass) {
+                uint32_t ci = pass ? it.csr_ext : it.csr_plain;
+                if (ci == kNone) continue;
+                const DevCSR& r = c.csrs[ci];
+                if (e.obj >= r.n_rows) continue;
+                ++rows;
+                if (direct) {
+                  uint32_t p = row_find(r, e.obj, s.sid, probes);
+                  if (p != kNone && visible(r, p, c.now_us)) {
+                    uint32_t cond = e.cond | (r.is_ext ? (r.cav[p] != 0) : 0u);
+                    set_found(c, e.q, cond);
+                    if (!cond) done = true;
+                  }
+                }
+                if (wild && !done) {
+                  uint32_t b = r.off[e.obj], en = r.off[e.obj + 1];
+                  ++probes;
+                  if (en > b && r.nbr[en - 1] == kWildcard && visible(r, en - 1, c.now_us)) {
+                    uint32_t cond = e.cond | (r.is_ext ? (r.cav[en - 1] != 0) : 0u);
+                    set_found(c, e.q, cond);
+                    if (!cond) done = true;
+                  }
+                }
+              }
+            }
+            // pass 2: userset subjects are re-dispatched
+            for (uint32_t k = 0; k < nd.count && !done; ++k) {
+              const DevItem it = c.items[nd.first + k];
+              if (it.srel == kEllipsis) continue;
+              emit_segment(c, it.csr_plain, e.obj, e.q, it.target, e.depth + 1u, e.cond, rows);
+              emit_segment(c, it.csr_ext, e.obj, e.q, it.target, e.depth + 1u, e.cond, rows);
+            }
+            break;
+          }
+          case NK_UNION: {
+            for (uint32_t k = 0; k < nd.count; ++k) {
+              const DevItem it = c.items[nd.first + k];
+              if (it.kind == IT_COMPUTED) {
+                push_entry(c, e.q, e.obj, it.target, e.depth + 1u, e.cond);
+              } else if (it.kind == IT_ARROW) {
+                emit_segment(c, it.csr_plain, e.obj, e.q, it.target, e.depth + 1u, e.cond, rows);
+                emit_segment(c, it.csr_ext, e.obj, e.q, it.target, e.depth + 1u, e.cond, rows);
+              } else if (it.kind == IT_SUB) {
+                spawn_join(c, e.q, e.obj, it.target, e.depth, e.cond, rows);
+              }
+            }
+            break;
+          }
+          case NK_INTERSECT:
+          case NK_EXCLUDE:
+          case NK_ARROW_ALL:
+            spawn_join(c, e.q, e.obj, e.node, e.depth, e.cond, rows);
+            break;
+          default:
+            break;
+        }
+      }
+    }
+  }
+  wave_add(&c.ctr->row_lookups, rows);
+  wave_add(&c.ctr->probes, probes);
+  wave_add(&c.ctr->expanded, expanded);
+}
+
+// Load-balanced edge enumeration: edge e belongs to the last segment whose edge_start <= e.
+__global__ void __launch_bounds__(kBlock) k_edges(Ctx c) {
+  const unsigned long long packed = c.ctr->seg_ctr;
+  const uint32_t nseg = (uint32_t)min((unsigned long long)(packed >> 40), (unsigned long long)c.seg_cap);
+  const unsigned long long total = packed & ((1ull << 40) - 1);
+  unsigned long long done_edges = 0, ext_edges = 0;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long eid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+       eid < total; eid += stride) {
+    uint32_t lo = 0, hi = nseg;  // upper_bound
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (c.segs[mid].edge_start <= eid) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == 0) continue;
+    const Segment s = c.segs[lo - 1];
+    const unsigned long long off = eid - s.edge_start;
+    if (off >= s.len) continue;  // a segment dropped on overflow
+    if (qflags(&c.queries[s.q]) & QF_DONE) continue;
+    const DevCSR& r = c.csrs[s.csr];
+    const uint32_t p = s.begin + (uint32_t)off;
+    const uint32_t x = r.nbr[p];
+    ++done_edges;
+    uint32_t cond = s.cond;
+    if (r.is_ext) {
+      ++ext_edges;
+      if (!visible(r, p, c.now_us)) continue;
+      cond |= (r.cav[p] != 0);
+    }
+    if (x == kWildcard) continue;
+    push_entry(c, s.q, x, s.target, s.depth, cond);
+  }
+  wave_add(&c.ctr->edges, done_edges);
+  wave_add(&c.ctr->ext_edges, ext_edges);
+}
+
+__device__ __forceinline__ uint32_t result_from_flags(uint32_t f) {
+  if (f & QF_FOUND_Y) return GCK_PERM_HAS;
+  if (f & QF_ERR) return kResErr;
+  if (f & QF_FOUND_C) return GCK_PERM_CONDITIONAL;
+  return GCK_PERM_NO;
+}
+
+__device__ __forceinline__ bool try_finalize(DevQuery* q, uint32_t res) {
+  uint32_t f = qflags(q);
+  while (!(f & QF_DONE)) {
+    uint32_t nf = f | QF_DONE | (res << QF_RES_SHIFT);
+    uint32_t prev = atomicCAS(&q->flags, f, nf);
+    if (prev == f) return true;
+    f = prev;
+  }
+  return false;
+}
+
+// Decide query `qi` with `res` and cascade the decision through its parent joins.
+__device__ void finalize(const Ctx& c, uint32_t qi, uint32_t res) {
+  for (int guard = 0; guard < 1 << 20; ++guard) {
+    DevQuery* q = &c.queries[qi];
+    if (!try_finalize(q, res)) return;
+    const uint32_t j = q->parent_join;
+    if (j == kNone) return;
+    DevJoin* J = &c.joins[j];
+    const uint32_t op = J->op;
+    uint32_t bit;
+    bool early;
+    if (op == NK_EXCLUDE && q->operand == 0) {
+      bit = res == GCK_PERM_HAS ? JS_BASE_Y : res == GCK_PERM_NO ? JS_BASE_N
+            : res == GCK_PERM_CONDITIONAL ? JS_BASE_C : JS_BASE_ERR;
+      early = res == GCK_PERM_NO;
+    } else {
+      bit = res == GCK_PERM_HAS ? JS_ANY_Y : res == GCK_PERM_NO ? JS_ANY_N
+            : res == GCK_PERM_CONDITIONAL ? JS_ANY_C : JS_ANY_ERR;
+      early = (op == NK_EXCLUDE) ? res == GCK_PERM_HAS : res == GCK_PERM_NO;
+    }
+    __hip_atomic_fetch_or(&J->state, bit, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    int rem = __hip_atomic_fetch_add(&J->remaining, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) - 1;
+    if (!(rem == 0 || early)) return;
+    uint32_t st = __hip_atomic_fetch_or(&J->state, (uint32_t)JS_RESOLVED, __ATOMIC_ACQ_REL,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    if (st & JS_RESOLVED) return;
+    uint32_t jr;
+    if (early) {
+      jr = GCK_PERM_NO;
+    } else if (op == NK_EXCLUDE) {
+      jr = (st & (JS_BASE_N | JS_ANY_Y)) ? GCK_PERM_NO
+           : (st & (JS_BASE_ERR | JS_ANY_ERR)) ? kResErr
+           : (st & (JS_BASE_C | JS_ANY_C)) ? GCK_PERM_CONDITIONAL : GCK_PERM_HAS;
+    } else {
+      jr = (st & JS_ANY_N) ? GCK_PERM_NO : (st & JS_ANY_ERR) ? kResErr
+           : (st & JS_ANY_C) ? GCK_PERM_CONDITIONAL : GCK_PERM_HAS;
+    }
+    if (rem > 0) {  // decided early: cancel the operands still running
+      for (uint32_t k = 0; k < J->n_ops; ++k) {
+        DevQuery* cq = &c.queries[J->first_child + k];
+        uint32_t f = qflags(cq);
+        while (!(f & QF_DONE)) {
+          uint32_t prev = atomicCAS(&cq->flags, f, f | QF_DONE | QF_CANCELLED);
+          if (prev == f) break;
+          f = prev;
+        }
+      }
+    }
+    if (J->cond && jr == GCK_PERM_HAS) jr = GCK_PERM_CONDITIONAL;  // caveated edge AND result
+    DevQuery* P = &c.queries[J->parent_q];
+    uint32_t fbit = jr == GCK_PERM_HAS ? QF_FOUND_Y : jr == GCK_PERM_CONDITIONAL ? QF_FOUND_C
+                    : jr == kResErr ? QF_ERR : 0u;
+    if (fbit) __hip_atomic_fetch_or(&P->flags, fbit, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    int pend = __hip_atomic_fetch_add(&P->pending_joins, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) - 1;
+    uint32_t pf = qflags(P);
+    if (pf & QF_DONE) return;
+    if (pf & QF_FOUND_Y) {
+      qi = J->parent_q;
+      res = GCK_PERM_HAS;
+      continue;
+    }
+    if (pend == 0 && P->last_alive <= c.level) {
+      qi = J->parent_q;
+      res = result_from_flags(pf);
+      continue;
+    }
+    return;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_resolve(Ctx c) {
+  // after an overflow some allocated queries/joins were never written: the batch is re-run
+  // split in half, so do not touch them
+  if (__hip_atomic_load(&c.ctr->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const uint32_t nq = min(__hip_atomic_load(&c.ctr->n_queries, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                          c.query_cap);
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x; qi < nq; qi += stride) {
+    DevQuery* q = &c.queries[qi];
+    uint32_t f = qflags(q);
+    if (f & QF_DONE) continue;
+    if (f & QF_FOUND_Y) {
+      finalize(c, qi, GCK_PERM_HAS);
+      continue;
+    }
+    if (q->last_alive > c.level) continue;  // entries pushed for the next level
+    int pend = __hip_atomic_load(&q->pending_joins, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (pend != 0) continue;
+    f = qflags(q);
+    finalize(c, qi, result_from_flags(f));
+  }
+}
+
+// Publish this level's counts and reset the per-level counters (one lane, after k_resolve).
+__global__ void k_level_end(DevCounters* ctr) {
+  unsigned long long packed = ctr->seg_ctr;
+  ctr->segs_total += packed >> 40;
+  ctr->last_next = ctr->next_size;
+  ctr->next_size = 0;
+  ctr->seg_ctr = 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_final(const DevQuery* __restrict__ queries, uint32_t n,
+                                                  const int32_t* __restrict__ item_err,
+                                                  uint8_t* __restrict__ out_perm,
+                                                  int32_t* __restrict__ out_err,
+                                                  DevCounters* ctr) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t f = queries[i].flags;
+  uint32_t res = (f >> QF_RES_SHIFT) & 0xF;
+  int32_t err = item_err[i];
+  if (!(f & QF_DONE)) {
+    atomicOr(&ctr->overflow, 32u);  // invariant violated: an undecided check
+    res = kResErr;
+  }
+  if (err == GCK_ITEM_OK && res == kResErr) err = GCK_ITEM_ERR_MAX_DEPTH;
+  out_perm[i] = (err != GCK_ITEM_OK) ? (uint8_t)GCK_PERM_UNSPECIFIED : (uint8_t)res;
+  out_err[i] = err;
+}
+
+// ---- host side -----------------------------------------------------------------------------
+
+static uint32_t ceil_log2(uint64_t x) {
+  uint32_t b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
+
+template <class T>
+static T* dalloc(std::vector<void*>& list, size_t count, uint64_t* bytes = nullptr) {
+  void* p = nullptr;
+  size_t sz = std::max<size_t>(count, 1) * sizeof(T);
+  HIP_OK(hipMalloc(&p, sz));
+  list.push_back(p);
+  if (bytes) *bytes += sz;
+  return static_cast<T*>(p);
+}
+
+int device_init(Engine& e) {
+  if (e.device_ready) return 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    throw Error(GCK_E_NO_DEVICE, "no HIP device available (libgck requires an MI355X)");
+  if (e.cfg.device < 0 || e.cfg.device >= n) throw Error(GCK_E_INVALID_ARGUMENT, "bad device ordinal");
+  e.device = e.cfg.device;
+  e.device_ready = true;
+  return 0;
+}
+
+static void free_list(std::vector<void*>& list) {
+  for (void* p : list) (void)hipFree(p);
+  list.clear();
+}
+
+void device_free(Engine& e) {
+  if (e.dev) {
+    (void)hipSetDevice(e.device);
+    free_list(e.dev->allocs);
+    delete e.dev;
+    e.dev = nullptr;
+  }
+  if (e.ws) {
+    (void)hipSetDevice(e.device);
+    Workspace* w = e.ws;
+    free_list(w->allocs);
+    if (w->h_ctr) (void)hipHostFree(w->h_ctr);
+    if (w->ev0) (void)hipEventDestroy(w->ev0);
+    if (w->ev1) (void)hipEventDestroy(w->ev1);
+    if (w->ev2) (void)hipEventDestroy(w->ev2);
+    if (w->stream) (void)hipStreamDestroy(w->stream);
+    delete w;
+    e.ws = nullptr;
+  }
+}
+
+uint64_t device_bytes(const Engine& e) { return e.dev ? e.dev->bytes : 0; }
+
+void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
+  device_init(e);
+  HIP_OK(hipSetDevice(e.device));
+  Schema& sc = *e.schema;
+  auto* ds = new DeviceSnapshot();
+  try {
+    std::vector<DevCSR> table;
+    for (HostCSR& h : csrs) {
+      DevCSR d{};
+      d.n_rows = h.n_rows;
+      d.is_ext = h.ext ? 1u : 0u;
+      uint64_t ne = h.dev_off ? h.n_edges : h.nbr.size();
+      uint32_t* off = dalloc<uint32_t>(ds->allocs, (size_t)h.n_rows + 1, &ds->bytes);
+      uint32_t* nbr = dalloc<uint32_t>(ds->allocs, ne, &ds->bytes);
+      if (h.dev_off) {
+        HIP_OK(hipMemcpy(off, h.dev_off, ((size_t)h.n_rows + 1) * 4, hipMemcpyDeviceToDevice));
+        if (ne) HIP_OK(hipMemcpy(nbr, h.dev_nbr, ne * 4, hipMemcpyDeviceToDevice));
+      } else {
+        HIP_OK(hipMemcpy(off, h.off.data(), h.off.size() * 4, hipMemcpyHostToDevice));
+        if (ne) HIP_OK(hipMemcpy(nbr, h.nbr.data(), ne * 4, hipMemcpyHostToDevice));
+      }
+      d.off = off;
+      d.nbr = nbr;
+      if (h.ext) {
+        uint32_t* cav = dalloc<uint32_t>(ds->allocs, ne, &ds->bytes);
+        int64_t* ex = dalloc<int64_t>(ds->allocs, ne, &ds->bytes);
+        if (ne) {
+          HIP_OK(hipMemcpy(cav, h.cav.data(), ne * 4, hipMemcpyHostToDevice));
+          HIP_OK(hipMemcpy(ex, h.exp_us.data(), ne * 8, hipMemcpyHostToDevice));
+        }
+        d.cav = cav;
+        d.exp_us = ex;
+      }
+      table.push_back(d);
+    }
+    // link the node program to the CSR table
+    std::vector<DevItem> items = sc.items;
+    for (size_t i = 0; i < items.size(); ++i) {
+      DevItem& it = items[i];
+      if (it.kind != IT_KIND && it.kind != IT_ARROW) continue;
+      uint16_t rel = sc.item_rel[i];
+      for (size_t k = 0; k < csrs.size(); ++k) {
+        const HostCSR& h = csrs[k];
+        if (h.rel == rel && h.stype == it.stype && h.srel == it.srel) {
+          (h.ext ? it.csr_ext : it.csr_plain) = (uint32_t)k;
+        }
+      }
+    }
+    ds->n_nodes = (uint32_t)sc.nodes.size();
+    ds->n_items = (uint32_t)items.size();
+    ds->n_csrs = (uint32_t)table.size();
+    ds->n_types = (uint32_t)sc.types.size();
+    ds->n_rels = (uint32_t)sc.rels.size();
+    ds->nodes = dalloc<DevNode>(ds->allocs, sc.nodes.size(), &ds->bytes);
+    ds->items = dalloc<DevItem>(ds->allocs, items.size(), &ds->bytes);
+    ds->csrs = dalloc<DevCSR>(ds->allocs, table.size(), &ds->bytes);
+    ds->type_counts = dalloc<uint32_t>(ds->allocs, sc.types.size(), &ds->bytes);
+    HIP_OK(hipMemcpy(ds->nodes, sc.nodes.data(), sc.nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+    if (!items.empty())
+      HIP_OK(hipMemcpy(ds->items, items.data(), items.size() * sizeof(DevItem), hipMemcpyHostToDevice));
+    if (!table.empty())
+      HIP_OK(hipMemcpy(ds->csrs, table.data(), table.size() * sizeof(DevCSR), hipMemcpyHostToDevice));
+    std::vector<uint32_t> counts(sc.types.size());
+    for (size_t t = 0; t < counts.size(); ++t) counts[t] = e.interner[t].count;
+    HIP_OK(hipMemcpy(ds->type_counts, counts.data(), counts.size() * 4, hipMemcpyHostToDevice));
+    ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
+    if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
+    ds->q_bits = 31 - ds->node_bits;
+  } catch (...) {
+    free_list(ds->allocs);
+    delete ds;
+    throw;
+  }
+  if (e.dev) {
+    free_list(e.dev->allocs);
+    delete e.dev;
+  }
+  e.dev = ds;
+}
+
+static Workspace* ensure_workspace(Engine& e) {
+  if (e.ws) return e.ws;
+  HIP_OK(hipSetDevice(e.device));
+  auto* w = new Workspace();
+  try {
+    const gck_config& cf = e.cfg;
+    w->max_batch = cf.max_batch ? cf.max_batch : 65536;
+    w->frontier_cap = cf.frontier_capacity ? cf.frontier_capacity : (size_t)16 << 20;
+    w->seg_cap = cf.segment_capacity ? cf.segment_capacity : (size_t)8 << 20;
+    w->query_cap = cf.query_capacity ? cf.query_capacity : std::max<size_t>((size_t)4 << 20, w->max_batch * 4);
+    w->join_cap = std::max<size_t>(w->query_cap / 2, 1);
+    uint64_t vc = cf.visited_capacity ? cf.visited_capacity : (1ull << 26);
+    w->visited_cap = 1ull << ceil_log2(vc);
+    w->frontier_cap = std::max(w->frontier_cap, w->max_batch);
+    w->query_cap = std::max(w->query_cap, w->max_batch);
+    if (w->frontier_cap > 0xFFFFFFF0ull || w->query_cap > 0x7FFFFFFFull)
+      throw Error(GCK_E_INVALID_ARGUMENT, "workspace capacity too large");
+    w->checks = dalloc<DevCheck>(w->allocs, w->max_batch);
+    w->item_err = dalloc<int32_t>(w->allocs, w->max_batch);
+    w->queries = dalloc<DevQuery>(w->allocs, w->query_cap);
+    w->joins = dalloc<DevJoin>(w->allocs, w->join_cap);
+    w->fr[0] = dalloc<Entry>(w->allocs, w->frontier_cap);
+    w->fr[1] = dalloc<Entry>(w->allocs, w->frontier_cap);
+    w->segs = dalloc<Segment>(w->allocs, w->seg_cap);
+    w->visited = dalloc<unsigned long long>(w->allocs, w->visited_cap);
+    w->ctr = dalloc<DevCounters>(w->allocs, 1);
+    w->d_items = dalloc<gck_item>(w->allocs, w->max_batch);
+    w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
+    w->d_err = dalloc<int32_t>(w->allocs, w->max_batch);
+    HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters), hipHostMallocDefault));
+    HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&w->ev0));
+    HIP_OK(hipEventCreate(&w->ev1));
+    HIP_OK(hipEventCreate(&w->ev2));
+  } catch (...) {
+    free_list(w->allocs);
+    if (w->h_ctr) (void)hipHostFree(w->h_ctr);
+    delete w;
+    throw;
+  }
+  e.ws = w;
+  return w;
+}
+
+static bool next_pow2_fits(uint32_t bits_q, size_t query_cap) { return (1ull << bits_q) >= query_cap; }
+
+// Runs one batch (n <= max_batch). Returns false on a workspace overflow (caller splits).
+static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
+                      uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
+  DeviceSnapshot& ds = *e.dev;
+  Ctx c{};
+  c.nodes = ds.nodes;
+  c.items = ds.items;
+  c.csrs = ds.csrs;
+  c.type_counts = ds.type_counts;
+  c.n_types = ds.n_types;
+  c.n_rels = ds.n_rels;
+  c.checks = w.checks;
+  c.queries = w.queries;
+  c.joins = w.joins;
+  c.segs = w.segs;
+  c.visited = w.visited;
+  c.vmask = w.visited_cap - 1;
+  c.ctr = w.ctr;
+  c.frontier_cap = (uint32_t)w.frontier_cap;
+  c.seg_cap = (uint32_t)std::min<size_t>(w.seg_cap, (1u << 24) - 1);
+  uint32_t qcap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << ds.q_bits);
+  c.query_cap = qcap;
+  c.join_cap = (uint32_t)w.join_cap;
+  c.node_shift = 33;
+  c.q_shift = 33 + ds.node_bits;
+  c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
+  c.now_us = now_us;
+  (void)next_pow2_fits;
+
+  HIP_OK(hipEventRecord(w.ev0, st));
+  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
+  HIP_OK(hipMemsetAsync(w.visited, 0xFF, w.visited_cap * sizeof(unsigned long long), st));
+  DevCounters init{};
+  init.n_queries = n;
+  HIP_OK(hipMemcpyAsync(w.ctr, &init, sizeof(DevCounters), hipMemcpyHostToDevice, st));
+  const uint32_t grid_n = (n + kBlock - 1) / kBlock;
+  c.level = 0;
+  hipLaunchKernelGGL(k_init, dim3(grid_n), dim3(kBlock), 0, st, c, d_items, n, w.fr[0], w.item_err);
+  HIP_OK(hipGetLastError());
+
+  uint32_t n_cur = n;
+  int cur = 0;
+  const uint32_t level_cap = 64 * c.max_depth + 64;
+  float expand_ms = 0.f;
+  for (uint32_t level = 0; n_cur > 0; ++level) {
+    if (level > level_cap) throw Error(GCK_E_DEVICE, "level cap exceeded (engine invariant)");
+    c.level = level;
+    c.next = w.fr[cur ^ 1];
+    hipLaunchKernelGGL(k_expand, dim3((n_cur + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c,
+                       w.fr[cur], n_cur);
+    hipLaunchKernelGGL(k_edges, dim3(2048), dim3(kBlock), 0, st, c);
+    hipLaunchKernelGGL(k_resolve, dim3(1024), dim3(kBlock), 0, st, c);
+    hipLaunchKernelGGL(k_level_end, dim3(1), dim3(1), 0, st, w.ctr);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (w.h_ctr->overflow) return false;
+    n_cur = w.h_ctr->last_next;
+    cur ^= 1;
+    e.stats.levels++;
+  }
+  hipLaunchKernelGGL(k_final, dim3(grid_n), dim3(kBlock), 0, st, w.queries, n, w.item_err, d_perm,
+                     d_err, w.ctr);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(w.ev1, st));
+  HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (w.h_ctr->overflow & 31u) return false;
+  if (w.h_ctr->overflow & 32u) throw Error(GCK_E_DEVICE, "engine invariant violated: undecided check");
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, w.ev0, w.ev1));
+  *ms_out += ms;
+  (void)expand_ms;
+  const DevCounters& h = *w.h_ctr;
+  e.stats.entries_expanded += h.expanded;
+  e.stats.row_lookups += h.row_lookups;
+  e.stats.membership_probes += h.probes;
+  e.stats.edges_enumerated += h.edges;
+  e.stats.ext_edges += h.ext_edges;
+  e.stats.queries += h.n_queries;
+  e.stats.joins += h.n_joins;
+  e.stats.batches++;
+  return true;
+}
+
+static void check_range(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us,
+                        uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms) {
+  size_t pos = 0;
+  while (pos < n) {
+    size_t len = std::min(n - pos, w.max_batch);
+    while (!run_batch(e, w, d_items + pos, (uint32_t)len, now_us, d_perm + pos, d_err + pos, st, ms)) {
+      e.stats.retries++;
+      if (len == 1) throw Error(GCK_E_CAPACITY, "device workspace overflow on a single check");
+      len = (len + 1) / 2;
+    }
+    pos += len;
+  }
+}
+
+static int64_t wall_now_us() {
+  using namespace std::chrono;
+  return duration_cast<microseconds>(system_clock::now().time_since_epoch()).count();
+}
+
+void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
+                  int32_t* d_err, void* stream) {
+  HIP_OK(hipSetDevice(e.device));
+  std::lock_guard<std::mutex> lk(e.ws_mu);
+  Workspace& w = *ensure_workspace(e);
+  hipStream_t st = stream ? (hipStream_t)stream : w.stream;
+  if (now_us == 0) now_us = wall_now_us();
+  float ms = 0.f;
+  check_range(e, w, d_items, n, now_us, d_perm, d_err, st, &ms);
+  e.stats.kernel_ms = ms;
+}
+
+void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
+                       int32_t* err) {
+  HIP_OK(hipSetDevice(e.device));
+  std::lock_guard<std::mutex> lk(e.ws_mu);
+  Workspace& w = *ensure_workspace(e);
+  if (now_us == 0) now_us = wall_now_us();
+  float ms = 0.f;
+  size_t pos = 0;
+  while (pos < n) {
+    size_t len = std::min(n - pos, w.max_batch);
+    HIP_OK(hipMemcpyAsync(w.d_items, items + pos, len * sizeof(gck_item), hipMemcpyHostToDevice, w.stream));
+    check_range(e, w, w.d_items, len, now_us, w.d_perm, w.d_err, w.stream, &ms);
+    HIP_OK(hipMemcpyAsync(perm + pos, w.d_perm, len, hipMemcpyDeviceToHost, w.stream));
+    HIP_OK(hipMemcpyAsync(err + pos, w.d_err, len * 4, hipMemcpyDeviceToHost, w.stream));
+    HIP_OK(hipStreamSynchronize(w.stream));
+    pos += len;
+  }
+  e.stats.kernel_ms = ms;
+}
+
+}  // namespace gck

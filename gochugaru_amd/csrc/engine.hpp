@@ -1,0 +1,154 @@
+// engine.hpp — host-side engine state: compiled schema, interner, snapshot staging and the
+// device-resident snapshot + workspace. Everything behind the C ABI in include/gck.h.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gck.h"
+#include "gck_internal.hpp"
+
+namespace gck {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// ---- schema IR ------------------------------------------------------------------------------
+struct Allowed {
+  uint16_t stype = 0;
+  uint16_t srel = kEllipsis;
+  bool wildcard = false;
+  bool expiration = false;
+  std::string caveat;
+};
+
+struct Expr {
+  enum Op { UNION, INTERSECT, EXCLUDE, NIL, COMPUTED, ARROW } op = NIL;
+  std::vector<Expr> kids;
+  std::string name;      // COMPUTED relation / ARROW target
+  std::string tupleset;  // ARROW tupleset relation
+  bool all = false;      // ARROW: .all()
+};
+
+struct RelDef {
+  std::string name;
+  uint16_t type = 0;
+  bool is_perm = false;
+  std::vector<Allowed> allowed;  // relation
+  Expr expr;                     // permission
+};
+
+struct TypeDef {
+  std::string name;
+  std::unordered_map<std::string, uint16_t> rels;  // name -> global relation id
+};
+
+struct CaveatDef {
+  std::string name;
+  std::vector<std::pair<std::string, std::string>> params;
+  std::string body;
+};
+
+struct Schema {
+  std::vector<TypeDef> types;
+  std::unordered_map<std::string, uint16_t> type_ids;
+  std::vector<RelDef> rels;
+  std::unordered_map<std::string, CaveatDef> caveats;
+  bool use_expiration = false;
+  // compiled node program; DevItem csr fields are linked at snapshot commit
+  std::vector<DevNode> nodes;
+  std::vector<DevItem> items;
+  std::vector<uint16_t> item_rel;  // relation whose CSR an IT_KIND/IT_ARROW item reads
+
+  int find_type(const std::string& n) const {
+    auto it = type_ids.find(n);
+    return it == type_ids.end() ? -1 : it->second;
+  }
+  int find_rel(uint16_t t, const std::string& n) const {
+    if (t >= types.size()) return -1;
+    auto it = types[t].rels.find(n);
+    return it == types[t].rels.end() ? -1 : it->second;
+  }
+};
+
+// Parses and validates SpiceDB schema DSL text, then compiles the node program.
+// Throws Error(GCK_E_SCHEMA, ...) on failure.
+std::unique_ptr<Schema> compile_schema(const std::string& text);
+
+// ---- interner -------------------------------------------------------------------------------
+struct TypeInterner {
+  std::unordered_map<std::string, uint32_t> ids;
+  std::vector<std::string> names;  // names[id] ("" for anonymous reserved ids)
+  uint32_t count = 0;              // ids [0, count) exist
+};
+
+// ---- snapshot staging -----------------------------------------------------------------------
+struct StagedTuple {
+  uint16_t rel, stype, srel, pad;
+  uint32_t obj, sid, cav;
+  int64_t exp_us;
+  uint64_t seq;  // arrival order: the last write of a duplicate wins (TOUCH)
+};
+
+struct HostCSR {
+  uint16_t rel, stype, srel;
+  bool ext;
+  uint32_t n_rows;
+  std::vector<uint32_t> off, nbr, cav;
+  std::vector<int64_t> exp_us;
+  // prebuilt device-resident input (gck_load_csr with GCK_MEM_DEVICE)
+  const uint32_t* dev_off = nullptr;
+  const uint32_t* dev_nbr = nullptr;
+  uint64_t n_edges = 0;
+};
+
+struct DeviceSnapshot;  // engine.hip
+struct Workspace;       // engine.hip
+
+struct Engine {
+  gck_config cfg{};
+  int device = 0;
+  bool device_ready = false;
+  std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
+  std::unique_ptr<Schema> schema;
+  std::vector<TypeInterner> interner;
+  std::vector<std::pair<std::string, std::string>> caveat_instances;  // [0] = none
+  // staging
+  bool staging = false;
+  uint64_t staged_revision = 0;
+  std::vector<StagedTuple> staged;
+  std::vector<HostCSR> prebuilt;
+  uint64_t seq = 0;
+  // committed
+  uint64_t revision = 0;
+  uint64_t n_tuples = 0;
+  bool committed = false;
+  DeviceSnapshot* dev = nullptr;
+  std::mutex ws_mu;
+  Workspace* ws = nullptr;
+  gck_stats stats{};
+  ~Engine();
+};
+
+// snapshot.cpp
+void add_tuples_text(Engine& e, const char* text, size_t len);
+std::vector<HostCSR> build_csrs(Engine& e);
+
+// engine.hip
+int device_init(Engine& e);
+void device_upload(Engine& e, std::vector<HostCSR>& csrs);
+void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
+                  uint8_t* d_perm, int32_t* d_err, void* stream);
+void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
+                       uint8_t* perm, int32_t* err);
+uint64_t device_bytes(const Engine& e);
+void device_free(Engine& e);
+
+}  // namespace gck

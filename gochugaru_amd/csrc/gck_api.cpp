@@ -1,0 +1,395 @@
+// gck_api.cpp — the extern "C" boundary (include/gck.h). Every entry point converts C++
+// exceptions into a negative status plus a thread-local message (gck_last_error).
+#include <cstring>
+#include <string>
+
+#include "engine.hpp"
+
+namespace gck {
+
+thread_local std::string g_last_error;
+
+Engine::~Engine() { device_free(*this); }
+
+uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json) {
+  if (!e.schema->caveats.count(name)) throw Error(GCK_E_INVALID_ARGUMENT, "unknown caveat '" + name + "'");
+  e.caveat_instances.emplace_back(name, json);
+  return (uint32_t)(e.caveat_instances.size() - 1);
+}
+
+void stage_tuple(Engine& e, const gck_tuple& t);
+
+}  // namespace gck
+
+using namespace gck;
+
+struct gck_engine {
+  Engine impl;
+};
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    g_last_error.clear();
+    return GCK_OK;
+  } catch (const Error& ex) {
+    g_last_error = ex.what();
+    return ex.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host out of memory";
+    return GCK_E_CAPACITY;
+  } catch (const std::exception& ex) {
+    g_last_error = ex.what();
+    return GCK_E_INVALID_ARGUMENT;
+  }
+}
+
+#define REQUIRE(cond, code, msg) \
+  do {                           \
+    if (!(cond)) throw Error(code, msg); \
+  } while (0)
+
+static Engine& need(gck_engine* e) {
+  REQUIRE(e, GCK_E_INVALID_ARGUMENT, "null engine");
+  return e->impl;
+}
+
+static Schema& need_schema(Engine& e) {
+  REQUIRE(e.schema, GCK_E_STATE, "no schema loaded (gck_load_schema)");
+  return *e.schema;
+}
+
+extern "C" {
+
+int gck_abi_version(void) { return GCK_ABI_VERSION; }
+
+const char* gck_last_error(void) { return g_last_error.c_str(); }
+
+int gck_create(const gck_config* cfg, gck_engine** out) {
+  return guard([&] {
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out pointer");
+    *out = nullptr;
+    auto* e = new gck_engine();
+    if (cfg) e->impl.cfg = *cfg;
+    if (e->impl.cfg.device < 0) {
+      delete e;
+      throw Error(GCK_E_INVALID_ARGUMENT, "bad device ordinal");
+    }
+    e->impl.caveat_instances.emplace_back("", "");
+    *out = e;
+  });
+}
+
+void gck_destroy(gck_engine* e) { delete e; }
+
+int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null schema text");
+    auto sc = compile_schema(std::string(text ? text : "", len));
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    e.schema = std::move(sc);
+    e.interner.assign(e.schema->types.size(), TypeInterner());
+    e.caveat_instances.assign(1, {"", ""});
+    e.staged.clear();
+    e.prebuilt.clear();
+    e.staging = false;
+    e.committed = false;
+    device_free(e);
+  });
+}
+
+int gck_type_id(gck_engine* ge, const char* name, size_t len, uint16_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out && (name || !len), GCK_E_INVALID_ARGUMENT, "null argument");
+    int t = need_schema(e).find_type(std::string(name, len));
+    REQUIRE(t >= 0, GCK_E_NOT_FOUND, "unknown type '" + std::string(name, len) + "'");
+    *out = (uint16_t)t;
+  });
+}
+
+int gck_relation_id(gck_engine* ge, uint16_t type, const char* name, size_t len, uint16_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out && (name || !len), GCK_E_INVALID_ARGUMENT, "null argument");
+    int r = need_schema(e).find_rel(type, std::string(name, len));
+    REQUIRE(r >= 0, GCK_E_NOT_FOUND, "unknown relation '" + std::string(name, len) + "'");
+    *out = (uint16_t)r;
+  });
+}
+
+int gck_type_count(gck_engine* ge, uint32_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = (uint32_t)need_schema(e).types.size();
+  });
+}
+
+int gck_relation_count(gck_engine* ge, uint32_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = (uint32_t)need_schema(e).rels.size();
+  });
+}
+
+int gck_intern(gck_engine* ge, uint16_t type, const char* const* ids, const uint32_t* lens, size_t n,
+               uint32_t flags, uint32_t* out_ids) {
+  return guard([&] {
+    Engine& e = need(ge);
+    Schema& sc = need_schema(e);
+    REQUIRE(type < sc.types.size(), GCK_E_INVALID_ARGUMENT, "unknown type id");
+    REQUIRE(n == 0 || (ids && lens && out_ids), GCK_E_INVALID_ARGUMENT, "null argument");
+    const bool create = flags & GCK_INTERN_CREATE;
+    std::unique_lock<std::shared_mutex> lk(e.mu, std::defer_lock);
+    std::shared_lock<std::shared_mutex> slk(e.mu, std::defer_lock);
+    if (create) lk.lock(); else slk.lock();
+    TypeInterner& ti = e.interner[type];
+    std::string key;
+    for (size_t i = 0; i < n; ++i) {
+      key.assign(ids[i], lens[i]);
+      if (key == "*") {
+        out_ids[i] = GCK_ID_WILDCARD;
+        continue;
+      }
+      auto it = ti.ids.find(key);
+      if (it != ti.ids.end()) {
+        out_ids[i] = it->second;
+      } else if (create) {
+        REQUIRE(ti.count < GCK_ID_ABSENT, GCK_E_CAPACITY, "too many objects of one type");
+        uint32_t id = ti.count++;
+        ti.ids.emplace(key, id);
+        if (ti.names.size() < ti.count) ti.names.resize(ti.count);
+        ti.names[id] = key;
+        out_ids[i] = id;
+      } else {
+        out_ids[i] = GCK_ID_ABSENT;
+      }
+    }
+  });
+}
+
+int gck_object_count(gck_engine* ge, uint16_t type, uint32_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(type < need_schema(e).types.size() && out, GCK_E_INVALID_ARGUMENT, "bad argument");
+    *out = e.interner[type].count;
+  });
+}
+
+int gck_reserve_objects(gck_engine* ge, uint16_t type, uint32_t n) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(type < need_schema(e).types.size(), GCK_E_INVALID_ARGUMENT, "bad type");
+    REQUIRE(n < GCK_ID_ABSENT, GCK_E_CAPACITY, "too many objects");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    TypeInterner& ti = e.interner[type];
+    if (n > ti.count) ti.count = n;
+  });
+}
+
+int gck_object_name(gck_engine* ge, uint16_t type, uint32_t id, char* buf, size_t cap, size_t* out_len) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(type < need_schema(e).types.size(), GCK_E_INVALID_ARGUMENT, "bad type");
+    TypeInterner& ti = e.interner[type];
+    REQUIRE(id < ti.count, GCK_E_NOT_FOUND, "unknown object id");
+    std::string nm = id < ti.names.size() && !ti.names[id].empty() ? ti.names[id] : std::to_string(id);
+    if (out_len) *out_len = nm.size();
+    if (buf && cap) {
+      size_t k = std::min(cap - 1, nm.size());
+      std::memcpy(buf, nm.data(), k);
+      buf[k] = 0;
+    }
+  });
+}
+
+int gck_add_caveat_instance(gck_engine* ge, const char* name, size_t name_len, const char* json,
+                            size_t json_len, uint32_t* out_id) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(name && out_id, GCK_E_INVALID_ARGUMENT, "null argument");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    *out_id = add_caveat_instance(e, std::string(name, name_len), std::string(json ? json : "", json_len));
+  });
+}
+
+int gck_begin_snapshot(gck_engine* ge, uint64_t revision) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    e.staging = true;
+    e.staged_revision = revision;
+    e.staged.clear();
+    e.prebuilt.clear();
+    e.seq = 0;
+  });
+}
+
+int gck_add_tuples(gck_engine* ge, const gck_tuple* tuples, size_t n) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
+    REQUIRE(n == 0 || tuples, GCK_E_INVALID_ARGUMENT, "null tuples");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    e.staged.reserve(e.staged.size() + n);
+    for (size_t i = 0; i < n; ++i) stage_tuple(e, tuples[i]);
+  });
+}
+
+int gck_add_tuples_text(gck_engine* ge, const char* text, size_t len) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
+    REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    add_tuples_text(e, text, len);
+  });
+}
+
+int gck_load_csr(gck_engine* ge, uint16_t relation, uint16_t subject_type, uint16_t subject_relation,
+                 uint32_t n_rows, const uint32_t* offsets, const uint32_t* neighbours, uint64_t n_edges,
+                 uint32_t mem_flags) {
+  return guard([&] {
+    Engine& e = need(ge);
+    Schema& sc = need_schema(e);
+    REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
+    REQUIRE(relation < sc.rels.size() && !sc.rels[relation].is_perm, GCK_E_INVALID_ARGUMENT,
+            "gck_load_csr: not a relation");
+    REQUIRE(subject_type < sc.types.size(), GCK_E_INVALID_ARGUMENT, "gck_load_csr: bad subject type");
+    bool allowed = false;
+    for (const Allowed& a : sc.rels[relation].allowed)
+      if (a.stype == subject_type && a.srel == subject_relation) allowed = true;
+    REQUIRE(allowed, GCK_E_INVALID_ARGUMENT, "gck_load_csr: subject kind not allowed by the schema");
+    REQUIRE(offsets && (neighbours || !n_edges), GCK_E_INVALID_ARGUMENT, "gck_load_csr: null arrays");
+    REQUIRE(n_edges < 0xFFFFFFFFull, GCK_E_CAPACITY, "gck_load_csr: more than 2^32-1 edges in one CSR");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    HostCSR h;
+    h.rel = relation;
+    h.stype = subject_type;
+    h.srel = subject_relation;
+    h.ext = false;
+    h.n_rows = n_rows;
+    h.n_edges = n_edges;
+    if (mem_flags & GCK_MEM_DEVICE) {
+      h.dev_off = offsets;
+      h.dev_nbr = neighbours;
+    } else {
+      REQUIRE(offsets[n_rows] == n_edges && offsets[0] == 0, GCK_E_INVALID_ARGUMENT,
+              "gck_load_csr: offsets do not span the neighbour array");
+      h.off.assign(offsets, offsets + (size_t)n_rows + 1);
+      h.nbr.assign(neighbours, neighbours + n_edges);
+    }
+    e.prebuilt.push_back(std::move(h));
+  });
+}
+
+int gck_commit_snapshot(gck_engine* ge) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    std::vector<HostCSR> csrs = build_csrs(e);
+    device_upload(e, csrs);  // device-pointer CSRs are copied before the caller regains control
+    e.staged.clear();
+    e.staged.shrink_to_fit();
+    e.staging = false;
+    e.revision = e.staged_revision;
+    e.committed = true;
+  });
+}
+
+int gck_revision(gck_engine* ge, uint64_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = e.revision;
+  });
+}
+
+int gck_tuple_count(gck_engine* ge, uint64_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = e.n_tuples;
+  });
+}
+
+int gck_device_bytes(gck_engine* ge, uint64_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = device_bytes(e);
+  });
+}
+
+static void check_consistency(Engine& e, const gck_consistency* cs) {
+  if (!cs) return;
+  switch (cs->requirement) {
+    case GCK_CONSISTENCY_MIN_LATENCY:
+    case GCK_CONSISTENCY_FULL:  // the local snapshot is the head of this evaluator
+      return;
+    case GCK_CONSISTENCY_AT_LEAST:
+      REQUIRE(e.revision >= cs->revision, GCK_E_REVISION,
+              "snapshot revision " + std::to_string(e.revision) + " is older than the requested " +
+                  std::to_string(cs->revision));
+      return;
+    case GCK_CONSISTENCY_SNAPSHOT:
+      REQUIRE(e.revision == cs->revision, GCK_E_REVISION,
+              "snapshot revision " + std::to_string(e.revision) + " != requested " +
+                  std::to_string(cs->revision));
+      return;
+    default:
+      throw Error(GCK_E_INVALID_ARGUMENT, "unknown consistency requirement");
+  }
+}
+
+int gck_check_bulk(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                   int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    check_consistency(e, cs);
+    if (n == 0) return;  // empty request -> empty response (client/client_test.go:203-207)
+    device_check_host(e, items, n, now_us, out_perm, out_err);
+  });
+}
+
+int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us,
+                          uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    if (n == 0) return;
+    device_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream);
+  });
+}
+
+int gck_last_stats(gck_engine* ge, gck_stats* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = e.stats;
+  });
+}
+
+int gck_reset_stats(gck_engine* ge) {
+  return guard([&] {
+    Engine& e = need(ge);
+    e.stats = gck_stats{};
+  });
+}
+
+}  // extern "C"

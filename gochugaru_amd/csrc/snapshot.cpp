@@ -1,0 +1,309 @@
+// snapshot.cpp — host-side ingest: canonical relationship text -> interned tuples -> CSR.
+//
+// Ingest record = rel.Relationship (rel/relationship.go:28-38) as streamed by
+// Client.ExportRelationships (client/client.go:472-499); text form = Relationship.String
+// (rel/relationship.go:51-90). The builder groups tuples per (relation, subject kind) and
+// splits plain edges from caveated/expiring ones (separate "ext" CSR with caveat ids and
+// expiry times), sorts every row ascending (wildcard id 0xFFFFFFFF sorts last) and keeps the
+// last write of a duplicate relationship (TOUCH semantics).
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace gck {
+namespace {
+
+// days since 1970-01-01 for a proleptic Gregorian date (H. Hinnant's algorithm)
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+
+bool parse_num(const std::string& s, size_t& i, int digits, int64_t& out) {
+  out = 0;
+  for (int k = 0; k < digits; ++k, ++i) {
+    if (i >= s.size() || !isdigit((unsigned char)s[i])) return false;
+    out = out * 10 + (s[i] - '0');
+  }
+  return true;
+}
+
+// RFC 3339 timestamp -> unix microseconds
+int64_t parse_rfc3339(const std::string& s) {
+  size_t i = 0;
+  int64_t Y, M, D, h, m, sec;
+  auto bad = [&]() -> Error { return Error(GCK_E_INVALID_ARGUMENT, "bad expiration timestamp '" + s + "'"); };
+  if (!parse_num(s, i, 4, Y) || s[i++] != '-' || !parse_num(s, i, 2, M) || s[i++] != '-' ||
+      !parse_num(s, i, 2, D) || (s[i] != 'T' && s[i] != 't') || !parse_num(s, ++i, 2, h) ||
+      s[i++] != ':' || !parse_num(s, i, 2, m) || s[i++] != ':' || !parse_num(s, i, 2, sec))
+    throw bad();
+  int64_t frac_us = 0;
+  if (i < s.size() && s[i] == '.') {
+    ++i;
+    int64_t scale = 100000;
+    while (i < s.size() && isdigit((unsigned char)s[i])) {
+      frac_us += (s[i] - '0') * scale;
+      scale /= 10;
+      ++i;
+    }
+  }
+  int64_t off_s = 0;
+  if (i < s.size() && (s[i] == 'Z' || s[i] == 'z')) {
+    ++i;
+  } else if (i < s.size() && (s[i] == '+' || s[i] == '-')) {
+    int sign = s[i++] == '-' ? -1 : 1;
+    int64_t oh, om;
+    if (!parse_num(s, i, 2, oh) || s[i++] != ':' || !parse_num(s, i, 2, om)) throw bad();
+    off_s = sign * (oh * 3600 + om * 60);
+  } else {
+    throw bad();
+  }
+  if (i != s.size()) throw bad();
+  int64_t days = days_from_civil(Y, (unsigned)M, (unsigned)D);
+  return ((days * 86400 + h * 3600 + m * 60 + sec) - off_s) * 1000000 + frac_us;
+}
+
+uint32_t intern_one(Engine& e, uint16_t type, const std::string& id) {
+  if (id == "*") return kWildcard;
+  TypeInterner& ti = e.interner[type];
+  auto it = ti.ids.find(id);
+  if (it != ti.ids.end()) return it->second;
+  if (ti.count >= kAbsent) throw Error(GCK_E_CAPACITY, "too many objects of one type");
+  uint32_t nid = ti.count++;
+  ti.ids.emplace(id, nid);
+  if (ti.names.size() < ti.count) ti.names.resize(ti.count);
+  ti.names[nid] = id;
+  return nid;
+}
+
+// Finds the end of a JSON value starting at s[i] ('{'), honouring strings and nesting.
+size_t json_end(const std::string& s, size_t i) {
+  int depth = 0;
+  bool str = false;
+  for (; i < s.size(); ++i) {
+    char c = s[i];
+    if (str) {
+      if (c == '\\') ++i;
+      else if (c == '"') str = false;
+      continue;
+    }
+    if (c == '"') str = true;
+    else if (c == '{' || c == '[') ++depth;
+    else if (c == '}' || c == ']') {
+      if (--depth == 0) return i + 1;
+    }
+  }
+  throw Error(GCK_E_INVALID_ARGUMENT, "unterminated caveat context");
+}
+
+}  // namespace
+
+uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json);
+
+void stage_tuple(Engine& e, const gck_tuple& t) {
+  const Schema& sc = *e.schema;
+  if (t.resource_type >= sc.types.size() || t.subject_type >= sc.types.size())
+    throw Error(GCK_E_INVALID_ARGUMENT, "tuple references an unknown type");
+  if (t.relation >= sc.rels.size() || sc.rels[t.relation].type != t.resource_type)
+    throw Error(GCK_E_INVALID_ARGUMENT, "tuple relation is not defined on its resource type");
+  const RelDef& rd = sc.rels[t.relation];
+  if (rd.is_perm)
+    throw Error(GCK_E_INVALID_ARGUMENT, "cannot write a relationship to permission '" + rd.name + "'");
+  bool ok = false;
+  for (const Allowed& a : rd.allowed) {
+    if (a.stype != t.subject_type) continue;
+    if (t.subject_id == kWildcard) {
+      if (a.wildcard && t.subject_relation == kEllipsis) ok = true;
+    } else if (!a.wildcard && a.srel == t.subject_relation) {
+      ok = true;
+    }
+  }
+  if (!ok)
+    throw Error(GCK_E_INVALID_ARGUMENT, "subject type/relation not allowed on '" +
+                                            sc.types[rd.type].name + "#" + rd.name + "'");
+  if (t.resource_id >= e.interner[t.resource_type].count ||
+      (t.subject_id != kWildcard && t.subject_id >= e.interner[t.subject_type].count))
+    throw Error(GCK_E_INVALID_ARGUMENT, "tuple references an object id that was never interned");
+  if (t.caveat >= e.caveat_instances.size())
+    throw Error(GCK_E_INVALID_ARGUMENT, "unknown caveat instance id");
+  StagedTuple s{};
+  s.rel = t.relation;
+  s.stype = t.subject_type;
+  s.srel = t.subject_relation;
+  s.obj = t.resource_id;
+  s.sid = t.subject_id;
+  s.cav = t.caveat;
+  s.exp_us = t.expires_at_us;
+  s.seq = e.seq++;
+  e.staged.push_back(s);
+}
+
+// One canonical line: type:id#rel@type:id[#rel][caveat[:{json}]][expiration:T]
+void add_tuples_text(Engine& e, const char* text, size_t len) {
+  const Schema& sc = *e.schema;
+  size_t pos = 0;
+  while (pos < len) {
+    size_t nl = pos;
+    while (nl < len && text[nl] != '\n') ++nl;
+    std::string line(text + pos, nl - pos);
+    pos = nl + 1;
+    while (!line.empty() && (line.back() == '\r' || line.back() == ' ' || line.back() == '\t')) line.pop_back();
+    size_t st = 0;
+    while (st < line.size() && (line[st] == ' ' || line[st] == '\t')) ++st;
+    line = line.substr(st);
+    if (line.empty() || line[0] == '#' || line.compare(0, 2, "//") == 0) continue;
+    auto bad = [&](const char* why) {
+      return Error(GCK_E_INVALID_ARGUMENT, std::string(why) + ": '" + line + "'");
+    };
+    size_t at = line.find('@');
+    if (at == std::string::npos) throw bad("invalid subject");
+    std::string res = line.substr(0, at);
+    size_t hash = res.find('#');
+    if (hash == std::string::npos || hash + 1 == res.size()) throw bad("invalid relation");
+    std::string rname = res.substr(hash + 1);
+    res = res.substr(0, hash);
+    size_t colon = res.find(':');
+    if (colon == std::string::npos) throw bad("invalid resource");
+    std::string rtype = res.substr(0, colon), rid = res.substr(colon + 1);
+    // subject ends at the first '['
+    std::string rest = line.substr(at + 1);
+    size_t br = rest.find('[');
+    std::string subj = br == std::string::npos ? rest : rest.substr(0, br);
+    std::string tail = br == std::string::npos ? std::string() : rest.substr(br);
+    std::string srel_name;
+    size_t sh = subj.find('#');
+    if (sh != std::string::npos) {
+      srel_name = subj.substr(sh + 1);
+      subj = subj.substr(0, sh);
+    }
+    size_t sc_ = subj.find(':');
+    if (sc_ == std::string::npos) throw bad("invalid subject");
+    std::string stype = subj.substr(0, sc_), sid = subj.substr(sc_ + 1);
+    // optional [caveat[:{json}]] then optional [expiration:T]
+    std::string cav_name, cav_json;
+    int64_t exp_us = 0;
+    size_t i = 0;
+    while (i < tail.size()) {
+      if (tail[i] != '[') throw bad("malformed trailer");
+      size_t j = i + 1;
+      while (j < tail.size() && tail[j] != ':' && tail[j] != ']') ++j;
+      if (j >= tail.size()) throw bad("malformed trailer");
+      std::string name = tail.substr(i + 1, j - i - 1);
+      if (name == "expiration") {
+        size_t k = tail.find(']', j);
+        if (k == std::string::npos) throw bad("malformed expiration");
+        exp_us = parse_rfc3339(tail.substr(j + 1, k - j - 1));
+        if (exp_us == 0) exp_us = 1;  // 0 is the "never" sentinel
+        i = k + 1;
+      } else {
+        cav_name = name;
+        if (tail[j] == ':') {
+          size_t k = json_end(tail, j + 1);
+          cav_json = tail.substr(j + 1, k - j - 1);
+          j = k;
+        }
+        if (j >= tail.size() || tail[j] != ']') throw bad("malformed caveat");
+        i = j + 1;
+      }
+    }
+    int rt = sc.find_type(rtype), stt = sc.find_type(stype);
+    if (rt < 0 || stt < 0) throw bad("unknown type");
+    int rr = sc.find_rel((uint16_t)rt, rname);
+    if (rr < 0) throw bad("unknown relation");
+    uint16_t srel = kEllipsis;
+    if (!srel_name.empty() && srel_name != "...") {
+      int x = sc.find_rel((uint16_t)stt, srel_name);
+      if (x < 0) throw bad("unknown subject relation");
+      srel = (uint16_t)x;
+    }
+    gck_tuple t{};
+    t.resource_type = (uint16_t)rt;
+    t.relation = (uint16_t)rr;
+    t.resource_id = intern_one(e, (uint16_t)rt, rid);
+    t.subject_type = (uint16_t)stt;
+    t.subject_relation = srel;
+    t.subject_id = intern_one(e, (uint16_t)stt, sid);
+    t.caveat = cav_name.empty() ? 0 : add_caveat_instance(e, cav_name, cav_json);
+    t.expires_at_us = exp_us;
+    stage_tuple(e, t);
+  }
+}
+
+std::vector<HostCSR> build_csrs(Engine& e) {
+  const Schema& sc = *e.schema;
+  std::vector<StagedTuple>& v = e.staged;
+  std::sort(v.begin(), v.end(), [](const StagedTuple& a, const StagedTuple& b) {
+    if (a.rel != b.rel) return a.rel < b.rel;
+    if (a.stype != b.stype) return a.stype < b.stype;
+    if (a.srel != b.srel) return a.srel < b.srel;
+    if (a.obj != b.obj) return a.obj < b.obj;
+    if (a.sid != b.sid) return a.sid < b.sid;
+    return a.seq < b.seq;
+  });
+  // keep the last write per (rel, stype, srel, obj, sid)
+  size_t w = 0;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (i + 1 < v.size() && v[i + 1].rel == v[i].rel && v[i + 1].stype == v[i].stype &&
+        v[i + 1].srel == v[i].srel && v[i + 1].obj == v[i].obj && v[i + 1].sid == v[i].sid)
+      continue;
+    v[w++] = v[i];
+  }
+  v.resize(w);
+  e.n_tuples = w;
+
+  std::vector<HostCSR> out;
+  size_t i = 0;
+  while (i < v.size()) {
+    size_t j = i;
+    while (j < v.size() && v[j].rel == v[i].rel && v[j].stype == v[i].stype && v[j].srel == v[i].srel) ++j;
+    const uint32_t n_rows = e.interner[sc.rels[v[i].rel].type].count;
+    for (int ext = 0; ext < 2; ++ext) {
+      HostCSR h;
+      h.rel = v[i].rel;
+      h.stype = v[i].stype;
+      h.srel = v[i].srel;
+      h.ext = ext == 1;
+      h.n_rows = n_rows;
+      h.off.assign((size_t)n_rows + 1, 0);
+      for (size_t k = i; k < j; ++k) {
+        bool is_ext = v[k].cav != 0 || v[k].exp_us != 0;
+        if (is_ext == h.ext) h.off[v[k].obj + 1]++;
+      }
+      std::partial_sum(h.off.begin(), h.off.end(), h.off.begin());
+      if (h.off.back() == 0) continue;
+      h.nbr.reserve(h.off.back());
+      for (size_t k = i; k < j; ++k) {  // already sorted by (obj, sid)
+        bool is_ext = v[k].cav != 0 || v[k].exp_us != 0;
+        if (is_ext != h.ext) continue;
+        h.nbr.push_back(v[k].sid);
+        if (h.ext) {
+          h.cav.push_back(v[k].cav);
+          h.exp_us.push_back(v[k].exp_us);
+        }
+      }
+      out.push_back(std::move(h));
+    }
+    i = j;
+  }
+  // prebuilt CSRs (gck_load_csr)
+  for (HostCSR& p : e.prebuilt) {
+    for (const HostCSR& h : out)
+      if (h.rel == p.rel && h.stype == p.stype && h.srel == p.srel && !h.ext)
+        throw Error(GCK_E_INVALID_ARGUMENT, "a CSR was loaded for a subject kind that also has staged tuples");
+    if (p.n_rows != e.interner[sc.rels[p.rel].type].count)
+      throw Error(GCK_E_INVALID_ARGUMENT, "prebuilt CSR row count does not match the type's object count");
+    e.n_tuples += p.dev_off ? p.n_edges : p.nbr.size();
+    out.push_back(std::move(p));
+  }
+  e.prebuilt.clear();
+  return out;
+}
+
+}  // namespace gck

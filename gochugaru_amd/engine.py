@@ -1,0 +1,373 @@
+"""ctypes binding of ``libgck.so`` (the C ABI in ``include/gck.h``).
+
+This is the host-side plumbing a Python caller uses; a Go caller binds the same symbols with
+cgo. The shared library is built in-tree by ``__graft_entry__.build()``
+(``make -C gochugaru_amd/csrc``). There is deliberately **no fallback**: if the library or a
+HIP device is missing, the calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgck.so")
+
+# ---- constants mirrored from include/gck.h ------------------------------------------------
+GCK_OK = 0
+GCK_E_INVALID_ARGUMENT = -1
+GCK_E_SCHEMA = -2
+GCK_E_NOT_FOUND = -3
+GCK_E_DEVICE = -4
+GCK_E_CAPACITY = -5
+GCK_E_STATE = -6
+GCK_E_REVISION = -7
+GCK_E_NO_DEVICE = -8
+
+PERM_UNSPECIFIED, PERM_NO, PERM_HAS, PERM_CONDITIONAL = 0, 1, 2, 3
+
+ITEM_OK = 0
+ITEM_ERR_MAX_DEPTH = 1
+ITEM_ERR_UNKNOWN_PERMISSION = 2
+ITEM_ERR_UNKNOWN_TYPE = 3
+ITEM_ERR_UNKNOWN_SUBJECT_RELATION = 4
+ITEM_ERR_WILDCARD_SUBJECT = 5
+
+ELLIPSIS = 0xFFFF
+ID_WILDCARD = 0xFFFFFFFF
+ID_ABSENT = 0xFFFFFFFE
+TYPE_INVALID = 0xFFFF
+REL_INVALID = 0xFFFE  # an id no schema relation has (never equal to ELLIPSIS)
+
+CONSISTENCY_MIN_LATENCY, CONSISTENCY_FULL, CONSISTENCY_AT_LEAST, CONSISTENCY_SNAPSHOT = 0, 1, 2, 3
+INTERN_CREATE = 1
+MEM_DEVICE = 1
+
+ITEM_DTYPE = np.dtype([
+    ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
+    ("subject_type", "<u2"), ("subject_relation", "<u2"), ("subject_id", "<u4"),
+    ("context_slot", "<u4"),
+])
+assert ITEM_DTYPE.itemsize == 20
+
+TUPLE_DTYPE = np.dtype({
+    "names": ["resource_type", "relation", "resource_id", "subject_type", "subject_relation",
+              "subject_id", "caveat", "expires_at_us"],
+    "formats": ["<u2", "<u2", "<u4", "<u2", "<u2", "<u4", "<u4", "<i8"],
+    "offsets": [0, 2, 4, 8, 10, 12, 16, 24],
+    "itemsize": 32,
+})
+
+ITEM_ERROR_MESSAGES = {
+    ITEM_ERR_MAX_DEPTH: "max depth exceeded: this usually indicates a recursive or too deep data dependency",
+    ITEM_ERR_UNKNOWN_PERMISSION: "relation/permission not found",
+    ITEM_ERR_UNKNOWN_TYPE: "object definition not found",
+    ITEM_ERR_UNKNOWN_SUBJECT_RELATION: "subject relation not found",
+    ITEM_ERR_WILDCARD_SUBJECT: "cannot perform check on wildcard subject",
+}
+
+
+class GckError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"gck error {code}: {message}")
+        self.code = code
+        self.message = message
+
+
+class _Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_depth", C.c_uint32), ("max_batch", C.c_uint32),
+                ("flags", C.c_uint32), ("visited_capacity", C.c_uint64),
+                ("frontier_capacity", C.c_uint64), ("segment_capacity", C.c_uint64),
+                ("query_capacity", C.c_uint64)]
+
+
+class _Consistency(C.Structure):
+    _fields_ = [("requirement", C.c_int32), ("reserved", C.c_uint32), ("revision", C.c_uint64)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("levels", C.c_uint64), ("entries_expanded", C.c_uint64),
+                ("row_lookups", C.c_uint64), ("membership_probes", C.c_uint64),
+                ("edges_enumerated", C.c_uint64), ("ext_edges", C.c_uint64),
+                ("queries", C.c_uint64), ("joins", C.c_uint64), ("retries", C.c_uint64),
+                ("kernel_ms", C.c_double), ("expand_ms", C.c_double)]
+
+
+# symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
+_P = C.c_void_p
+_SIGS = {
+    "gck_abi_version": (C.c_int, []),
+    "gck_last_error": (C.c_char_p, []),
+    "gck_create": (C.c_int, [C.POINTER(_Config), C.POINTER(_P)]),
+    "gck_destroy": (None, [_P]),
+    "gck_load_schema": (C.c_int, [_P, C.c_char_p, C.c_size_t]),
+    "gck_type_id": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint16)]),
+    "gck_relation_id": (C.c_int, [_P, C.c_uint16, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint16)]),
+    "gck_type_count": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    "gck_relation_count": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    "gck_intern": (C.c_int, [_P, C.c_uint16, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32),
+                             C.c_size_t, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gck_object_count": (C.c_int, [_P, C.c_uint16, C.POINTER(C.c_uint32)]),
+    "gck_reserve_objects": (C.c_int, [_P, C.c_uint16, C.c_uint32]),
+    "gck_object_name": (C.c_int, [_P, C.c_uint16, C.c_uint32, C.c_char_p, C.c_size_t,
+                                  C.POINTER(C.c_size_t)]),
+    "gck_add_caveat_instance": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                          C.POINTER(C.c_uint32)]),
+    "gck_begin_snapshot": (C.c_int, [_P, C.c_uint64]),
+    "gck_add_tuples": (C.c_int, [_P, _P, C.c_size_t]),
+    "gck_add_tuples_text": (C.c_int, [_P, C.c_char_p, C.c_size_t]),
+    "gck_load_csr": (C.c_int, [_P, C.c_uint16, C.c_uint16, C.c_uint16, C.c_uint32, _P, _P,
+                               C.c_uint64, C.c_uint32]),
+    "gck_commit_snapshot": (C.c_int, [_P]),
+    "gck_revision": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_tuple_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_device_bytes": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_check_bulk": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.c_int64, _P, _P]),
+    "gck_check_bulk_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
+    "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
+    "gck_reset_stats": (C.c_int, [_P]),
+}
+
+_lib = None
+
+
+def load_library(path: str = _LIB_PATH):
+    """Load libgck.so (raises if it has not been built — there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libgck.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (make -C gochugaru_amd/csrc); the check engine has no CPU fallback")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != GCK_OK:
+        msg = _lib.gck_last_error().decode("utf-8", "replace")
+        raise GckError(rc, msg)
+
+
+class Stats(dict):
+    pass
+
+
+class Engine:
+    """One engine = one device-resident snapshot on one GPU (``gck_engine``)."""
+
+    def __init__(self, device: int = 0, max_depth: int = 50, max_batch: int = 65536,
+                 visited_capacity: int = 0, frontier_capacity: int = 0,
+                 segment_capacity: int = 0, query_capacity: int = 0):
+        lib = load_library()
+        cfg = _Config(device, max_depth, max_batch, 0, visited_capacity, frontier_capacity,
+                      segment_capacity, query_capacity)
+        h = _P()
+        _check(lib.gck_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self._lib = lib
+        self._type_ids = {}
+        self._rel_ids = {}
+
+    def close(self):
+        if self._h:
+            self._lib.gck_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- schema --------------------------------------------------------------------------
+    def load_schema(self, text: str):
+        b = text.encode()
+        _check(self._lib.gck_load_schema(self._h, b, len(b)))
+        self._type_ids.clear()
+        self._rel_ids.clear()
+
+    def type_id(self, name: str) -> int:
+        """Type id, or TYPE_INVALID if the type is not defined."""
+        t = self._type_ids.get(name)
+        if t is None:
+            out = C.c_uint16()
+            b = name.encode()
+            rc = self._lib.gck_type_id(self._h, b, len(b), C.byref(out))
+            if rc == GCK_E_NOT_FOUND:
+                return TYPE_INVALID
+            _check(rc)
+            t = self._type_ids[name] = out.value
+        return t
+
+    def relation_id(self, type_id: int, name: str) -> int:
+        """Global relation id, or REL_INVALID if not defined on the type."""
+        key = (type_id, name)
+        r = self._rel_ids.get(key)
+        if r is None:
+            if type_id == TYPE_INVALID:
+                return REL_INVALID
+            out = C.c_uint16()
+            b = name.encode()
+            rc = self._lib.gck_relation_id(self._h, type_id, b, len(b), C.byref(out))
+            if rc == GCK_E_NOT_FOUND:
+                return REL_INVALID
+            _check(rc)
+            r = self._rel_ids[key] = out.value
+        return r
+
+    def counts(self) -> Tuple[int, int]:
+        t, r = C.c_uint32(), C.c_uint32()
+        _check(self._lib.gck_type_count(self._h, C.byref(t)))
+        _check(self._lib.gck_relation_count(self._h, C.byref(r)))
+        return t.value, r.value
+
+    # ---- interning -----------------------------------------------------------------------
+    def intern(self, type_id: int, ids: Sequence[str], create: bool = False) -> np.ndarray:
+        n = len(ids)
+        out = np.empty(n, dtype=np.uint32)
+        if n == 0:
+            return out
+        enc = [s.encode() for s in ids]
+        arr = (C.c_char_p * n)(*enc)
+        lens = (C.c_uint32 * n)(*[len(b) for b in enc])
+        _check(self._lib.gck_intern(self._h, type_id, arr, lens, n,
+                                    INTERN_CREATE if create else 0,
+                                    out.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return out
+
+    def object_count(self, type_id: int) -> int:
+        out = C.c_uint32()
+        _check(self._lib.gck_object_count(self._h, type_id, C.byref(out)))
+        return out.value
+
+    def reserve_objects(self, type_id: int, n: int):
+        _check(self._lib.gck_reserve_objects(self._h, type_id, n))
+
+    def object_name(self, type_id: int, oid: int) -> str:
+        buf = C.create_string_buffer(1100)
+        ln = C.c_size_t()
+        _check(self._lib.gck_object_name(self._h, type_id, oid, buf, len(buf), C.byref(ln)))
+        return buf.value.decode()
+
+    def add_caveat_instance(self, name: str, context_json: str = "") -> int:
+        out = C.c_uint32()
+        nb, jb = name.encode(), context_json.encode()
+        _check(self._lib.gck_add_caveat_instance(self._h, nb, len(nb), jb, len(jb), C.byref(out)))
+        return out.value
+
+    # ---- snapshot ------------------------------------------------------------------------
+    def begin_snapshot(self, revision: int):
+        _check(self._lib.gck_begin_snapshot(self._h, revision))
+
+    def add_tuples_text(self, text: str):
+        b = text.encode()
+        _check(self._lib.gck_add_tuples_text(self._h, b, len(b)))
+
+    def add_tuples(self, tuples: np.ndarray):
+        tuples = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+        _check(self._lib.gck_add_tuples(self._h, tuples.ctypes.data, len(tuples)))
+
+    def load_csr(self, relation: int, subject_type: int, subject_relation: int, n_rows: int,
+                 offsets, neighbours, n_edges: int, device: bool = False):
+        """Bulk ingest of one prebuilt CSR. Host numpy arrays (uint32) or, with device=True,
+        raw device pointers (ints) on the engine's GPU."""
+        if device:
+            po, pn = int(offsets), int(neighbours)
+        else:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+            neighbours = np.ascontiguousarray(neighbours, dtype=np.uint32)
+            po, pn = offsets.ctypes.data, neighbours.ctypes.data
+        _check(self._lib.gck_load_csr(self._h, relation, subject_type, subject_relation, n_rows,
+                                      po, pn, n_edges, MEM_DEVICE if device else 0))
+
+    def commit_snapshot(self):
+        _check(self._lib.gck_commit_snapshot(self._h))
+
+    def load_snapshot_text(self, revision: int, text: str):
+        self.begin_snapshot(revision)
+        self.add_tuples_text(text)
+        self.commit_snapshot()
+
+    @property
+    def revision(self) -> int:
+        out = C.c_uint64()
+        _check(self._lib.gck_revision(self._h, C.byref(out)))
+        return out.value
+
+    @property
+    def tuple_count(self) -> int:
+        out = C.c_uint64()
+        _check(self._lib.gck_tuple_count(self._h, C.byref(out)))
+        return out.value
+
+    @property
+    def device_bytes(self) -> int:
+        out = C.c_uint64()
+        _check(self._lib.gck_device_bytes(self._h, C.byref(out)))
+        return out.value
+
+    # ---- checks --------------------------------------------------------------------------
+    def check_bulk(self, items: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY,
+                   revision: int = 0, now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+        items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
+        n = len(items)
+        perm = np.zeros(n, dtype=np.uint8)
+        err = np.zeros(n, dtype=np.int32)
+        cs = _Consistency(requirement, 0, revision)
+        _check(self._lib.gck_check_bulk(self._h, C.byref(cs), items.ctypes.data if n else None, n,
+                                        now_us, perm.ctypes.data if n else None,
+                                        err.ctypes.data if n else None))
+        return perm, err
+
+    def check_bulk_device(self, d_items: int, n: int, d_perm: int, d_err: int,
+                          stream: Optional[int] = None, now_us: int = 0):
+        _check(self._lib.gck_check_bulk_device(self._h, d_items, n, now_us, d_perm, d_err,
+                                               stream))
+
+    def stats(self) -> Stats:
+        s = _Stats()
+        _check(self._lib.gck_last_stats(self._h, C.byref(s)))
+        return Stats({k: getattr(s, k) for k, _ in _Stats._fields_})
+
+    def reset_stats(self):
+        _check(self._lib.gck_reset_stats(self._h))
+
+    # ---- string-level convenience --------------------------------------------------------
+    def make_items(self, rels: Iterable) -> np.ndarray:
+        """rel.Relationship-like items -> interned gck_item array (unknown names map to
+        invalid ids so the device reports the per-item error; unknown ids map to ABSENT)."""
+        rels = list(rels)
+        items = np.zeros(len(rels), dtype=ITEM_DTYPE)
+        by_type = {}
+        for i, r in enumerate(rels):
+            rt = self.type_id(r.ResourceType)
+            st = self.type_id(r.SubjectType)
+            items[i]["resource_type"] = rt
+            items[i]["permission"] = self.relation_id(rt, r.ResourceRelation)
+            items[i]["subject_type"] = st
+            items[i]["subject_relation"] = (ELLIPSIS if r.SubjectRelation in ("", "...")
+                                            else self.relation_id(st, r.SubjectRelation))
+            if rt != TYPE_INVALID:
+                by_type.setdefault(rt, ([], []))[0].append(i)
+            if st != TYPE_INVALID:
+                by_type.setdefault(st, ([], []))[1].append(i)
+        for t, (ri, si) in by_type.items():
+            if ri:
+                items["resource_id"][ri] = self.intern(t, [rels[i].ResourceID for i in ri])
+            if si:
+                items["subject_id"][si] = self.intern(t, [rels[i].SubjectID for i in si])
+        for i, r in enumerate(rels):
+            if items[i]["resource_type"] == TYPE_INVALID:
+                items[i]["resource_id"] = ID_ABSENT
+            if items[i]["subject_type"] == TYPE_INVALID:
+                items[i]["subject_id"] = ID_WILDCARD if r.SubjectID == "*" else ID_ABSENT
+        return items

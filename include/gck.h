@@ -1,0 +1,198 @@
+/*
+ * gck.h — C ABI of the MI355X batched permission-check engine (libgck.so).
+ *
+ * This is the drop-in boundary for gochugaru's check path. A Go caller binds
+ * it through cgo; the Python host mirror (gochugaru_amd/engine.py) binds it
+ * through ctypes. Signatures use plain pointers and sizes only.
+ *
+ * Reference interfaces replaced (authzed/gochugaru @ 2025-10-03):
+ *   gck_check_bulk / gck_check_bulk_device
+ *       replace the CheckBulkPermissions round-trip made by Client.Check
+ *       (client/client.go:261-266) and consumed at client/client.go:271-283; transitively
+ *       CheckOne/CheckAny/CheckAll/CheckIter (client/client.go:129-180).
+ *   gck_load_schema
+ *       consumes the schema text returned by Client.ReadSchema (client/client.go:416-422).
+ *   gck_begin_snapshot / gck_add_tuples / gck_add_tuples_text / gck_load_csr / gck_commit_snapshot
+ *       consume the relationships streamed by Client.ExportRelationships at the schema's
+ *       revision (client/client.go:472-499, rel.FromV1Proto rel/relationship.go:147-172).
+ *   gck_intern
+ *       replaces the per-item string handling of Client.Check's item loop
+ *       (client/client.go:242-259) with batched string -> dense u32 interning.
+ *   gck_revision / gck_check_bulk's consistency argument
+ *       honour consistency.Strategy (consistency/consistency.go:15-77) as sent in
+ *       CheckBulkPermissionsRequest.Consistency (client/client.go:263).
+ *
+ * Ownership: all inputs and outputs are caller-allocated; the engine never retains a caller
+ * pointer after a call returns. Return value: GCK_OK (0) or a negative GCK_E_* status; the
+ * message is available from gck_last_error() (thread-local).
+ * Threading: gck_check_bulk* may be called concurrently; snapshot/schema calls are exclusive.
+ */
+#ifndef GCK_H
+#define GCK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCK_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define GCK_OK 0
+#define GCK_E_INVALID_ARGUMENT (-1) /* gRPC InvalidArgument */
+#define GCK_E_SCHEMA (-2)           /* schema text failed to parse/validate */
+#define GCK_E_NOT_FOUND (-3)        /* unknown type/relation name in a lookup */
+#define GCK_E_DEVICE (-4)           /* HIP failure: map to gRPC Unavailable (caller retries) */
+#define GCK_E_CAPACITY (-5)         /* a device workspace limit was exceeded */
+#define GCK_E_STATE (-6)            /* wrong call order (no schema / no snapshot) */
+#define GCK_E_REVISION (-7)         /* consistency requirement not satisfiable locally */
+#define GCK_E_NO_DEVICE (-8)        /* no HIP device / HIP runtime unavailable */
+
+/* ---- Permissionship (authzed v1 CheckPermissionResponse.Permissionship) --------------- */
+#define GCK_PERM_UNSPECIFIED 0
+#define GCK_PERM_NO 1
+#define GCK_PERM_HAS 2
+#define GCK_PERM_CONDITIONAL 3
+
+/* ---- per-item errors (CheckBulkPermissionsPair.Error) --------------------------------- */
+#define GCK_ITEM_OK 0
+#define GCK_ITEM_ERR_MAX_DEPTH 1                /* dispatch depth budget exhausted */
+#define GCK_ITEM_ERR_UNKNOWN_PERMISSION 2       /* permission not defined on the type */
+#define GCK_ITEM_ERR_UNKNOWN_TYPE 3             /* resource or subject type not defined */
+#define GCK_ITEM_ERR_UNKNOWN_SUBJECT_RELATION 4 /* subject relation not defined */
+#define GCK_ITEM_ERR_WILDCARD_SUBJECT 5         /* subject id "*" is not checkable */
+
+/* ---- special ids ---------------------------------------------------------------------- */
+#define GCK_ELLIPSIS 0xFFFFu          /* subject relation "..." (a concrete object) */
+#define GCK_ID_WILDCARD 0xFFFFFFFFu   /* subject id "*" */
+#define GCK_ID_ABSENT 0xFFFFFFFEu     /* an id that is not in the snapshot */
+#define GCK_TYPE_INVALID 0xFFFFu
+
+/* ---- consistency requirement (consistency.Strategy) ------------------------------------ */
+#define GCK_CONSISTENCY_MIN_LATENCY 0
+#define GCK_CONSISTENCY_FULL 1
+#define GCK_CONSISTENCY_AT_LEAST 2
+#define GCK_CONSISTENCY_SNAPSHOT 3
+
+/* ---- flags ---------------------------------------------------------------------------- */
+#define GCK_INTERN_CREATE 1u     /* gck_intern: create ids for unseen strings */
+#define GCK_MEM_DEVICE 1u        /* gck_load_csr: pointers are device memory */
+
+typedef struct gck_engine gck_engine;
+
+typedef struct gck_config {
+  int32_t device;              /* HIP device ordinal */
+  uint32_t max_depth;          /* dispatch depth budget; 0 = 50 (SpiceDB default) */
+  uint32_t max_batch;          /* checks per device launch sequence; 0 = 65536 */
+  uint32_t flags;              /* reserved, 0 */
+  uint64_t visited_capacity;   /* slots of the per-batch visited hash (power of 2); 0 = auto */
+  uint64_t frontier_capacity;  /* entries per frontier buffer; 0 = auto */
+  uint64_t segment_capacity;   /* row segments per level; 0 = auto */
+  uint64_t query_capacity;     /* queries per batch (checks + sub-queries of joins); 0 = auto */
+} gck_config;
+
+/* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
+typedef struct gck_item {
+  uint16_t resource_type;
+  uint16_t permission;         /* global relation id (gck_relation_id) */
+  uint32_t resource_id;
+  uint16_t subject_type;
+  uint16_t subject_relation;   /* GCK_ELLIPSIS for a concrete object */
+  uint32_t subject_id;
+  uint32_t context_slot;       /* 0 = no check-time caveat context */
+} gck_item;                    /* 20 bytes */
+
+/* One relationship, interned: rel.Relationship (rel/relationship.go:28-38). */
+typedef struct gck_tuple {
+  uint16_t resource_type;
+  uint16_t relation;           /* global relation id */
+  uint32_t resource_id;
+  uint16_t subject_type;
+  uint16_t subject_relation;   /* GCK_ELLIPSIS or a relation id of subject_type */
+  uint32_t subject_id;         /* GCK_ID_WILDCARD for "type:*" */
+  uint32_t caveat;             /* caveat instance id from gck_add_caveat_instance; 0 = none */
+  int64_t expires_at_us;       /* unix microseconds; 0 = never */
+} gck_tuple;                   /* 32 bytes */
+
+typedef struct gck_consistency {
+  int32_t requirement;         /* GCK_CONSISTENCY_* */
+  uint32_t reserved;
+  uint64_t revision;           /* AT_LEAST / SNAPSHOT token, decoded */
+} gck_consistency;
+
+typedef struct gck_stats {
+  uint64_t batches;
+  uint64_t levels;             /* BFS levels (dispatch waves) executed */
+  uint64_t entries_expanded;   /* (query, object, node) entries expanded */
+  uint64_t row_lookups;        /* CSR rows opened (each = one 8-B offset pair) */
+  uint64_t membership_probes;  /* 4-B neighbour reads by membership binary searches */
+  uint64_t edges_enumerated;   /* 4-B neighbour reads by userset/arrow enumeration */
+  uint64_t ext_edges;          /* caveated/expiring edges read (+4 B caveat id +8 B expiry) */
+  uint64_t queries;            /* queries allocated (checks + join operands) */
+  uint64_t joins;              /* intersection/exclusion/all() joins spawned */
+  uint64_t retries;            /* batch splits after a workspace overflow */
+  double kernel_ms;            /* device time of the last batch (HIP events) */
+  double expand_ms;            /* device time of the last batch's expand kernels */
+} gck_stats;
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+int gck_abi_version(void);
+const char* gck_last_error(void);
+int gck_create(const gck_config* cfg, gck_engine** out);
+void gck_destroy(gck_engine* e);
+
+/* ---- schema (Client.ReadSchema text, client/client.go:416-422) ------------------------ */
+int gck_load_schema(gck_engine* e, const char* text, size_t len);
+int gck_type_id(gck_engine* e, const char* name, size_t len, uint16_t* out);
+int gck_relation_id(gck_engine* e, uint16_t type, const char* name, size_t len, uint16_t* out);
+int gck_type_count(gck_engine* e, uint32_t* out);
+int gck_relation_count(gck_engine* e, uint32_t* out);
+
+/* ---- interning (Client.Check item loop, client/client.go:242-259) --------------------- */
+int gck_intern(gck_engine* e, uint16_t type, const char* const* ids, const uint32_t* lens,
+               size_t n, uint32_t flags, uint32_t* out_ids);
+int gck_object_count(gck_engine* e, uint16_t type, uint32_t* out);
+/* Declares ids [0, n) of `type` as existing (anonymous objects for bulk CSR ingest). */
+int gck_reserve_objects(gck_engine* e, uint16_t type, uint32_t n);
+int gck_object_name(gck_engine* e, uint16_t type, uint32_t id, char* buf, size_t cap,
+                    size_t* out_len);
+
+/* ---- caveats (rel.Relationship.CaveatName/CaveatContext) ------------------------------ */
+int gck_add_caveat_instance(gck_engine* e, const char* name, size_t name_len,
+                            const char* context_json, size_t json_len, uint32_t* out_id);
+
+/* ---- snapshot ingest (Client.ExportRelationships, client/client.go:472-499) ----------- */
+int gck_begin_snapshot(gck_engine* e, uint64_t revision);
+int gck_add_tuples(gck_engine* e, const gck_tuple* tuples, size_t n);
+/* Canonical rel.Relationship.String lines (rel/relationship.go:51-90), '\n'-separated. */
+int gck_add_tuples_text(gck_engine* e, const char* text, size_t len);
+/* Prebuilt CSR for one (relation, subject kind): rows sorted ascending, no duplicates,
+ * plain edges only (no caveat/expiration). n_rows = object count of the relation's type. */
+int gck_load_csr(gck_engine* e, uint16_t relation, uint16_t subject_type,
+                 uint16_t subject_relation, uint32_t n_rows, const uint32_t* offsets,
+                 const uint32_t* neighbours, uint64_t n_edges, uint32_t mem_flags);
+int gck_commit_snapshot(gck_engine* e);
+int gck_revision(gck_engine* e, uint64_t* out);
+int gck_tuple_count(gck_engine* e, uint64_t* out);
+/* Bytes resident in HBM for the snapshot (CSR + tables). */
+int gck_device_bytes(gck_engine* e, uint64_t* out);
+
+/* ---- checks (CheckBulkPermissions, client/client.go:261-283) -------------------------- */
+/* Host buffers: items[n] in, out_perm[n] (GCK_PERM_*), out_err[n] (GCK_ITEM_*) out.
+ * `now_us` = the evaluation time for expiring relationships (unix microseconds; 0 = wall
+ * clock). Results are in request order. */
+int gck_check_bulk(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
+                   int64_t now_us, uint8_t* out_perm, int32_t* out_err);
+/* Device-resident buffers on the engine's device; `stream` is a hipStream_t (NULL = the
+ * engine's own stream). Returns after the results are written (stream synchronised). */
+int gck_check_bulk_device(gck_engine* e, const gck_item* d_items, size_t n, int64_t now_us,
+                          uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
+int gck_last_stats(gck_engine* e, gck_stats* out);
+int gck_reset_stats(gck_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCK_H */

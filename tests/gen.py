@@ -1,0 +1,248 @@
+"""Seeded synthetic schemas + relationship graphs for parity tests (small sizes: the Python
+oracle must finish in seconds). Every graph is acyclic so that parity is well-defined
+(SURVEY.md §5.1 item 9)."""
+import random
+
+GDOCS = """
+definition user {}
+definition group {
+  relation member: user | group#member
+}
+definition folder {
+  relation parent: folder
+  relation viewer: user | group#member
+  relation editor: user | group#member
+  permission edit = editor + parent->edit
+  permission view = viewer + edit + parent->view
+}
+definition doc {
+  relation parent: folder
+  relation owner: user
+  relation viewer: user | user:* | group#member
+  relation editor: user | group#member
+  permission edit = owner + editor + parent->edit
+  permission view = viewer + edit + parent->view
+}
+"""
+
+GITHUB = """
+definition user {}
+definition team {
+  relation maintainer: user
+  relation direct_member: user | team#member
+  permission member = maintainer + direct_member
+}
+definition org {
+  relation admin: user
+  relation member: user | team#member
+  permission is_member = admin + member
+}
+definition repo {
+  relation org: org
+  relation reader: user | team#member
+  relation writer: user | team#member
+  relation admin: user | team#member
+  relation banned: user
+  permission read = (reader + writer + admin + org->is_member) - banned
+  permission write = (writer + admin) & org->is_member
+  permission admin_all = org.all(is_member)
+}
+"""
+
+CAVEATED = """
+caveat only_on_tuesday(day_of_the_week string) {
+  day_of_the_week == "tuesday"
+}
+definition user {}
+definition group {
+  relation member: user | group#member | user with only_on_tuesday
+}
+definition doc {
+  relation viewer: user | group#member | user with only_on_tuesday | user with expiration
+  relation editor: user | user with expiration
+  permission edit = editor
+  permission view = viewer + edit
+  permission strict = viewer & editor
+}
+use expiration
+"""
+
+NESTED = """
+definition user {}
+definition group {
+  relation member: user | group#member
+}
+definition doc {
+  relation viewer: group#member
+  permission view = viewer
+}
+"""
+
+
+def _pick(rng, n):
+    return rng.randrange(n)
+
+
+def gdocs(seed, n_users=60, n_groups=25, n_folders=30, n_docs=60):
+    rng = random.Random(seed)
+    t = []
+    for g in range(n_groups):
+        for _ in range(rng.randint(0, 4)):
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}")
+        for _ in range(rng.randint(0, 2)):
+            h = rng.randrange(g + 1, n_groups + 1)
+            if h < n_groups:
+                t.append(f"group:g{g}#member@group:g{h}#member")
+    for f in range(n_folders):
+        if f > 0 and rng.random() < 0.8:
+            t.append(f"folder:f{f}#parent@folder:f{rng.randrange(f)}")
+        for rel in ("viewer", "editor"):
+            for _ in range(rng.randint(0, 2)):
+                if rng.random() < 0.5:
+                    t.append(f"folder:f{f}#{rel}@user:u{_pick(rng, n_users)}")
+                else:
+                    t.append(f"folder:f{f}#{rel}@group:g{_pick(rng, n_groups)}#member")
+    for d in range(n_docs):
+        if rng.random() < 0.8:
+            t.append(f"doc:d{d}#parent@folder:f{_pick(rng, n_folders)}")
+        if rng.random() < 0.5:
+            t.append(f"doc:d{d}#owner@user:u{_pick(rng, n_users)}")
+        for rel in ("viewer", "editor"):
+            for _ in range(rng.randint(0, 2)):
+                x = rng.random()
+                if x < 0.5:
+                    t.append(f"doc:d{d}#{rel}@user:u{_pick(rng, n_users)}")
+                elif x < 0.97 or rel == "editor":
+                    t.append(f"doc:d{d}#{rel}@group:g{_pick(rng, n_groups)}#member")
+                else:
+                    t.append(f"doc:d{d}#viewer@user:*")
+    checks = []
+    for _ in range(400):
+        x = rng.random()
+        if x < 0.45:
+            checks.append(f"doc:d{_pick(rng, n_docs + 3)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users + 3)}")
+        elif x < 0.75:
+            checks.append(f"folder:f{_pick(rng, n_folders)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users)}")
+        elif x < 0.9:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@user:u{_pick(rng, n_users)}")
+        else:
+            checks.append(f"doc:d{_pick(rng, n_docs)}#view@group:g{_pick(rng, n_groups)}#member")
+    return GDOCS, t, checks
+
+
+def github(seed, n_users=50, n_teams=20, n_orgs=6, n_repos=50):
+    rng = random.Random(seed)
+    t = []
+    for tm in range(n_teams):
+        for _ in range(rng.randint(0, 2)):
+            t.append(f"team:t{tm}#maintainer@user:u{_pick(rng, n_users)}")
+        for _ in range(rng.randint(0, 3)):
+            t.append(f"team:t{tm}#direct_member@user:u{_pick(rng, n_users)}")
+        if rng.random() < 0.5:
+            h = rng.randrange(tm + 1, n_teams + 1)
+            if h < n_teams:
+                t.append(f"team:t{tm}#direct_member@team:t{h}#member")
+    for o in range(n_orgs):
+        t.append(f"org:o{o}#admin@user:u{_pick(rng, n_users)}")
+        for _ in range(rng.randint(1, 6)):
+            if rng.random() < 0.6:
+                t.append(f"org:o{o}#member@user:u{_pick(rng, n_users)}")
+            else:
+                t.append(f"org:o{o}#member@team:t{_pick(rng, n_teams)}#member")
+    for r in range(n_repos):
+        for _ in range(rng.randint(1, 2)):
+            t.append(f"repo:r{r}#org@org:o{_pick(rng, n_orgs)}")
+        for rel in ("reader", "writer", "admin"):
+            for _ in range(rng.randint(0, 2)):
+                if rng.random() < 0.6:
+                    t.append(f"repo:r{r}#{rel}@user:u{_pick(rng, n_users)}")
+                else:
+                    t.append(f"repo:r{r}#{rel}@team:t{_pick(rng, n_teams)}#member")
+        if rng.random() < 0.3:
+            t.append(f"repo:r{r}#banned@user:u{_pick(rng, n_users)}")
+    checks = []
+    for _ in range(400):
+        x = rng.random()
+        if x < 0.8:
+            checks.append(f"repo:r{_pick(rng, n_repos)}#{rng.choice(['read', 'write', 'admin_all'])}@user:u{_pick(rng, n_users)}")
+        else:
+            checks.append(f"team:t{_pick(rng, n_teams)}#member@user:u{_pick(rng, n_users)}")
+    return GITHUB, t, checks
+
+
+def caveated(seed, n_users=40, n_groups=15, n_docs=40):
+    """Caveated and expiring tuples; ~half of the expiring ones are already expired at
+    NOW_US (2025-10-03)."""
+    rng = random.Random(seed)
+    t = []
+    past, future = "2020-01-01T00:00:00Z", "2999-01-01T00:00:00Z"
+    for g in range(n_groups):
+        for _ in range(rng.randint(0, 4)):
+            cav = "[only_on_tuesday]" if rng.random() < 0.2 else ""
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}{cav}")
+        if rng.random() < 0.5:
+            h = rng.randrange(g + 1, n_groups + 1)
+            if h < n_groups:
+                t.append(f"group:g{g}#member@group:g{h}#member")
+    for d in range(n_docs):
+        for _ in range(rng.randint(0, 3)):
+            x = rng.random()
+            u = _pick(rng, n_users)
+            if x < 0.3:
+                t.append(f"doc:d{d}#viewer@user:u{u}")
+            elif x < 0.5:
+                t.append(f"doc:d{d}#viewer@user:u{u}[only_on_tuesday]")
+            elif x < 0.6:
+                t.append(f'doc:d{d}#viewer@user:u{u}[only_on_tuesday:{{"day_of_the_week":"tuesday"}}]')
+            elif x < 0.75:
+                t.append(f"doc:d{d}#viewer@user:u{u}[expiration:{rng.choice([past, future])}]")
+            else:
+                t.append(f"doc:d{d}#viewer@group:g{_pick(rng, n_groups)}#member")
+        for _ in range(rng.randint(0, 2)):
+            u = _pick(rng, n_users)
+            if rng.random() < 0.5:
+                t.append(f"doc:d{d}#editor@user:u{u}")
+            else:
+                t.append(f"doc:d{d}#editor@user:u{u}[expiration:{rng.choice([past, future])}]")
+    # bias half of the checks towards subjects that appear on the document
+    users_of = {}
+    for s in t:
+        if s.startswith("doc:") and "@user:" in s:
+            d = s[4:s.index("#")]
+            u = s.split("@user:")[1].split("[")[0]
+            users_of.setdefault(d, []).append(u)
+    checks = []
+    for _ in range(300):
+        d = _pick(rng, n_docs)
+        perm = rng.choice(['view', 'edit', 'strict'])
+        if rng.random() < 0.6 and users_of.get(f"d{d}"):
+            u = rng.choice(users_of[f"d{d}"])
+        else:
+            u = f"u{_pick(rng, n_users)}"
+        checks.append(f"doc:d{d}#{perm}@user:{u}")
+    return CAVEATED, t, checks
+
+
+def nested(seed, n_users=200, n_groups=120, layers=8, n_docs=80):
+    """Layered group DAG (config 4 shape at toy scale)."""
+    rng = random.Random(seed)
+    t = []
+    per = n_groups // layers
+    for g in range(n_groups):
+        layer = g // per
+        for _ in range(rng.randint(0, 5)):
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}")
+        if layer + 1 < layers:
+            for _ in range(rng.randint(0, 3)):
+                h = (layer + 1) * per + _pick(rng, per)
+                if h < n_groups:
+                    t.append(f"group:g{g}#member@group:g{h}#member")
+    for d in range(n_docs):
+        for _ in range(rng.randint(1, 3)):
+            t.append(f"doc:d{d}#viewer@group:g{_pick(rng, per * 2)}#member")
+    checks = [f"doc:d{_pick(rng, n_docs)}#view@user:u{_pick(rng, n_users)}" for _ in range(400)]
+    return NESTED, t, checks
+
+
+FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested}
+NOW_US = 1759449600 * 1_000_000  # 2025-10-03T00:00:00Z

@@ -1,0 +1,135 @@
+"""C ABI checks that need no GPU: libgck.so loads, exports exactly what include/gck.h
+declares, and the host-side data plane (schema compiler, interner, text ingest validation)
+behaves. No compute calls are made here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gochugaru_amd import engine as E
+from tests.helpers import load_golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gck.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gck_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = E.load_library()
+    declared = header_functions()
+    assert len(declared) >= 25
+    for name in declared:
+        assert hasattr(lib, name), name
+    # the ctypes signature table covers the header exactly
+    assert sorted(E._SIGS) == declared
+
+
+def test_struct_layouts_match_header():
+    assert E.ITEM_DTYPE.itemsize == 20
+    assert E.TUPLE_DTYPE.itemsize == 32
+    assert C.sizeof(E._Config) == 48
+    assert E.load_library().gck_abi_version() == 1
+
+
+@pytest.fixture()
+def eng():
+    e = E.Engine(device=0)
+    yield e
+    e.close()
+
+
+def test_schema_compile_and_lookup(eng):
+    g = load_golden("semantics.json")["suites"][0]
+    eng.load_schema(g["schema"])
+    t, r = eng.counts()
+    assert t == 4 and r == 1 + 5 + 9
+    doc = eng.type_id("doc")
+    assert eng.relation_id(doc, "view") != E.REL_INVALID
+    assert eng.relation_id(doc, "nosuch") == E.REL_INVALID
+    assert eng.type_id("nosuch") == E.TYPE_INVALID
+
+
+@pytest.mark.parametrize("bad", [
+    "definition a { relation r: nosuch }",
+    "definition a { permission p = nosuch }",
+    "definition a {}\ndefinition a {}",
+    "definition a { relation r: a  permission p = r->missing }",
+    "definition a { relation r: a:*  permission p = r->p }",
+    "definition a { relation r: a with nocaveat }",
+    "definition a { relation r: a",
+    "definition a { permission p = (r }",
+])
+def test_schema_errors(eng, bad):
+    with pytest.raises(E.GckError) as ei:
+        eng.load_schema(bad)
+    assert ei.value.code == E.GCK_E_SCHEMA
+
+
+def test_intern_and_text_staging(eng):
+    g = load_golden("semantics.json")["suites"][0]
+    eng.load_schema(g["schema"])
+    eng.begin_snapshot(1)
+    eng.add_tuples_text("\n".join(g["tuples"]))
+    user = eng.type_id("user")
+    ids = eng.intern(user, ["alice", "bob", "nobody", "*"])
+    assert ids[0] != ids[1] and ids[2] == E.ID_ABSENT and ids[3] == E.ID_WILDCARD
+    assert eng.object_name(user, int(ids[0])) == "alice"
+    new = eng.intern(user, ["nobody"], create=True)
+    assert new[0] == eng.object_count(user) - 1
+    # validation: relationship to a permission, disallowed subject kind, unknown names
+    for bad in ["doc:x#view@user:a", "doc:x#owner@group:g#member", "doc:x#nosuch@user:a",
+                "nosuch:x#owner@user:a", "doc:x#owner@user:*", "doc:x#owner", "docx#owner@user:a"]:
+        with pytest.raises(E.GckError):
+            eng.add_tuples_text(bad)
+
+
+def test_text_trailers(eng):
+    g = load_golden("semantics.json")["suites"][2]
+    eng.load_schema(g["schema"])
+    eng.begin_snapshot(3)
+    eng.add_tuples_text("\n".join(g["tuples"]))
+    with pytest.raises(E.GckError):
+        eng.add_tuples_text("doc:a#viewer@user:u1[nosuchcaveat]")
+    with pytest.raises(E.GckError):
+        eng.add_tuples_text("doc:a#editor@user:u1[expiration:not-a-time]")
+
+
+def test_binary_tuple_staging(eng):
+    eng.load_schema("definition user {}\ndefinition group { relation member: user | group#member }")
+    user, group = eng.type_id("user"), eng.type_id("group")
+    member = eng.relation_id(group, "member")
+    eng.reserve_objects(user, 10)
+    eng.reserve_objects(group, 4)
+    eng.begin_snapshot(9)
+    t = np.zeros(3, dtype=E.TUPLE_DTYPE)
+    t["resource_type"] = group
+    t["relation"] = member
+    t["resource_id"] = [0, 1, 1]
+    t["subject_type"] = [user, user, group]
+    t["subject_relation"] = [E.ELLIPSIS, E.ELLIPSIS, member]
+    t["subject_id"] = [3, 4, 2]
+    eng.add_tuples(t)
+    t2 = t[:1].copy()
+    t2["subject_id"] = 99  # never reserved
+    with pytest.raises(E.GckError):
+        eng.add_tuples(t2)
+
+
+def test_state_errors(eng):
+    with pytest.raises(E.GckError) as ei:
+        eng.begin_snapshot(1)
+    assert ei.value.code == E.GCK_E_STATE
+    eng.load_schema("definition user {}")
+    with pytest.raises(E.GckError) as ei:
+        eng.add_tuples_text("user:a#x@user:b")
+    assert ei.value.code == E.GCK_E_STATE
+    with pytest.raises(E.GckError) as ei:
+        eng.check_bulk(np.zeros(1, dtype=E.ITEM_DTYPE))
+    assert ei.value.code == E.GCK_E_STATE

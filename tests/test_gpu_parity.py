@@ -1,0 +1,202 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's known answers, the
+hand-derived SpiceDB-semantics fixtures and the Python oracle on seeded random graphs.
+Bar: bit-exact tri-state (HAS / NO / CONDITIONAL) and per-item error codes."""
+import numpy as np
+import pytest
+
+from gochugaru_amd import consistency, rel
+from gochugaru_amd import engine as E
+from gochugaru_amd.client import Client, CheckItemError, OverlapKeyPanic, WithOverlapRequired
+from oracle import spicedb_ref as ref
+from tests import gen
+from tests.helpers import (expected_code, iso_to_unix, load_golden, oracle_for, parse_check,
+                           to_oracle_item)
+
+pytestmark = pytest.mark.gpu
+
+CLIENT = load_golden("client_check.json")
+FOUNDERS = load_golden("readme_founders.json")
+SEM = load_golden("semantics.json")
+NOW_US = int(iso_to_unix(SEM["now"]) * 1e6)
+
+
+def make_engine(schema, tuples, revision=1, **kw):
+    e = E.Engine(**kw)
+    e.load_schema(schema)
+    e.load_snapshot_text(revision, "\n".join(tuples))
+    return e
+
+
+def device_results(e, checks, now_us=NOW_US):
+    items = e.make_items([parse_check(s) for s in checks])
+    perm, err = e.check_bulk(items, now_us=now_us)
+    return [(int(p), int(x)) for p, x in zip(perm, err)]
+
+
+# ---- reference known answers (client/client_test.go:141-216, README.md:71-88) --------------
+
+@pytest.fixture(scope="module")
+def doc_client():
+    e = make_engine(CLIENT["schema"], CLIENT["tuples"])
+    yield Client(e)
+    e.close()
+
+
+@pytest.mark.parametrize("case", CLIENT["cases"], ids=lambda c: c["name"])
+def test_client_check_known_answers(doc_client, case):
+    cs = consistency.Full() if case["consistency"] == "full" else consistency.MinLatency()
+    results, err = doc_client.Check(None, cs, *[parse_check(s) for s in case["checks"]])
+    assert err is None
+    assert results == case["expected"]
+
+
+def test_check_one_any_all(doc_client):
+    ok, err = doc_client.CheckOne(None, consistency.MinLatency(),
+                                  rel.MustFromTriple("document:check_test1", "edit", "user:alice"))
+    assert (ok, err) == (True, None)
+    rs = [rel.MustFromTriple("document:check_test1", "edit", "user:bob"),
+          rel.MustFromTriple("document:check_test1", "view", "user:bob")]
+    assert doc_client.CheckAny(None, consistency.MinLatency(), *rs) == (True, None)
+    assert doc_client.CheckAll(None, consistency.MinLatency(), *rs) == (False, None)
+    assert doc_client.CheckAll(None, consistency.MinLatency()) == (True, None)  # vacuous
+    assert doc_client.CheckAny(None, consistency.MinLatency()) == (False, None)
+
+
+def test_check_iter_and_item_error(doc_client):
+    rs = [rel.MustFromTriple("document:check_test1", "view", "user:bob")] * 2500
+    out = list(doc_client.CheckIter(None, consistency.MinLatency(), iter(rs)))
+    assert len(out) == 2500 and all(v == (True, None) for v in out)
+    # the first per-item error stops the iteration (client/client.go:168-171)
+    bad = rs[:3] + [rel.MustFromTriple("document:README", "owner", "user:bot")] + rs[:3]
+    out = list(doc_client.CheckIter(None, consistency.MinLatency(), iter(bad), chunk=2))
+    assert out[:2] == [(True, None), (True, None)]
+    assert out[2][0] is False and isinstance(out[2][1], CheckItemError) and len(out) == 3
+    # Check returns the prefix before the error (client/client.go:279-280)
+    results, err = doc_client.Check(None, consistency.MinLatency(), *bad)
+    assert results == [True, True, True] and isinstance(err, CheckItemError)
+
+
+def test_overlap_required_panics():
+    # client/client_test.go:218-277
+    e = make_engine(CLIENT["schema"], CLIENT["tuples"])
+    c, _ = Client.NewWithOpts(e, WithOverlapRequired())
+    r = rel.MustFromTriple("document:README", "owner", "user:bot")
+    with pytest.raises(OverlapKeyPanic):
+        c.CheckOne(None, consistency.Full(), r)
+    c.CheckOne(consistency.WithOverlapKey(None, "test"), consistency.Full(), r)  # no panic
+    e.close()
+
+
+def test_consistency_revisions():
+    e = make_engine(CLIENT["schema"], CLIENT["tuples"], revision=7)
+    c = Client(e)
+    r = rel.MustFromTriple("document:check_test1", "edit", "user:alice")
+    assert c.CheckOne(None, consistency.AtLeast("7"), r) == (True, None)
+    assert c.CheckOne(None, consistency.Snapshot("7"), r) == (True, None)
+    ctx = consistency.Context(metadata={})
+    object.__setattr__(ctx, "deadline", 0)  # no retries
+    ok, err = c.CheckOne(ctx, consistency.AtLeast("8"), r)
+    assert ok is False and isinstance(err, E.GckError) and err.code == E.GCK_E_REVISION
+    ok, err = c.CheckOne(ctx, consistency.Snapshot("6"), r)
+    assert err is not None
+    e.close()
+
+
+def test_readme_founders():
+    e = make_engine(FOUNDERS["schema"], FOUNDERS["tuples"])
+    c = Client(e)
+    founders = [rel.FromTriple("company:authzed", "founder", "user:" + f) for f in ("jake", "joey", "jimmy")]
+    assert c.CheckAll(None, consistency.MinLatency(), *founders) == (True, None)
+    e.close()
+    e = make_engine(FOUNDERS["schema"], [t for t in FOUNDERS["tuples"] if t != FOUNDERS["negative_remove"]])
+    assert Client(e).CheckAll(None, consistency.MinLatency(), *founders) == (False, None)
+    e.close()
+
+
+# ---- hand-derived SpiceDB semantics (tests/golden/semantics.json) ---------------------------
+
+def _suite(name):
+    return next(s for s in SEM["suites"] if s["name"] == name)
+
+
+def test_semantics_rewrites():
+    s = _suite("gdocs-arrows-exclusion-intersection-wildcard")
+    e = make_engine(s["schema"], s["tuples"])
+    got = device_results(e, [c[0] for c in s["checks"]])
+    for (chk, label, note), g in zip(s["checks"], got):
+        assert g == expected_code(label), (chk, note)
+    e.close()
+
+
+def test_semantics_depth():
+    s = _suite("depth-budget")
+    for chk, depth, label, note in s["depth_checks"]:
+        e = make_engine(s["schema"], s["tuples"], max_depth=depth)
+        assert device_results(e, [chk]) == [expected_code(label)], (chk, depth, note)
+        e.close()
+
+
+def test_semantics_caveats_device_contract():
+    s = _suite("caveats-and-expiration")
+    e = make_engine(s["schema"], s["tuples"])
+    got = device_results(e, [c[0] for c in s["caveat_checks"]])
+    for c, g in zip(s["caveat_checks"], got):
+        assert g == expected_code(c[2]), c
+    e.close()
+
+
+# ---- random graphs vs the oracle -------------------------------------------------------------
+
+@pytest.mark.parametrize("family", sorted(gen.FAMILIES))
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_parity(family, seed):
+    schema, tuples, checks = gen.FAMILIES[family](seed)
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6, evaluate_caveats=False)
+    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+    e = make_engine(schema, tuples)
+    got = device_results(e, checks, now_us=gen.NOW_US)
+    bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
+    assert not bad, bad[:10]
+    e.close()
+
+
+def test_small_batches_and_overflow_retry():
+    schema, tuples, checks = gen.gdocs(11)
+    ck = oracle_for(schema, tuples)
+    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+    # tiny workspace: forces batch splits and overflow retries, results must not change
+    e = make_engine(schema, tuples, max_batch=37, frontier_capacity=64, segment_capacity=64,
+                    visited_capacity=256, query_capacity=64)
+    got = device_results(e, checks, now_us=gen.NOW_US)
+    assert got == want
+    st = e.stats()
+    assert st["batches"] >= len(checks) // 37
+    e.close()
+
+
+def test_determinism_and_empty():
+    schema, tuples, checks = gen.github(5)
+    e = make_engine(schema, tuples)
+    a = device_results(e, checks)
+    b = device_results(e, checks)
+    assert a == b
+    perm, err = e.check_bulk(np.zeros(0, dtype=E.ITEM_DTYPE))
+    assert len(perm) == 0 and len(err) == 0
+    e.close()
+
+
+def test_device_buffers_api():
+    import torch
+    schema, tuples, checks = gen.nested(4)
+    e = make_engine(schema, tuples)
+    items = e.make_items([parse_check(c) for c in checks])
+    want_p, want_e = e.check_bulk(items, now_us=gen.NOW_US)
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    d_perm = torch.zeros(len(items), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(len(items), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    e.check_bulk_device(d_items.data_ptr(), len(items), d_perm.data_ptr(), d_err.data_ptr(),
+                        stream=torch.cuda.current_stream().cuda_stream, now_us=gen.NOW_US)
+    assert np.array_equal(d_perm.cpu().numpy(), want_p)
+    assert np.array_equal(d_err.cpu().numpy(), want_e)
+    e.close()

@@ -1,0 +1,107 @@
+"""Pins the Python oracle (oracle/spicedb_ref.py) against the reference's known answers and
+the hand-derived SpiceDB-semantics fixtures. CPU only."""
+import pytest
+
+from oracle import spicedb_ref as ref
+from tests.helpers import (expected_code, iso_to_unix, load_golden, oracle_for, parse_check,
+                           to_oracle_item)
+
+CLIENT = load_golden("client_check.json")
+FOUNDERS = load_golden("readme_founders.json")
+SEM = load_golden("semantics.json")
+
+
+@pytest.mark.parametrize("case", CLIENT["cases"], ids=lambda c: c["name"])
+def test_client_check_known_answers(case):
+    # client/client_test.go:141-216 — HAS -> true, everything else false
+    ck = oracle_for(CLIENT["schema"], CLIENT["tuples"])
+    got = [ck.check(to_oracle_item(parse_check(s)))[0] == ref.HAS for s in case["checks"]]
+    assert got == case["expected"]
+
+
+def test_readme_founders():
+    ck = oracle_for(FOUNDERS["schema"], FOUNDERS["tuples"])
+    res = [ck.check(to_oracle_item(parse_check(s))) for s in FOUNDERS["checks"]]
+    assert all(p == ref.HAS and e == 0 for p, e in res) == FOUNDERS["expected_all"]
+    tuples = [t for t in FOUNDERS["tuples"] if t != FOUNDERS["negative_remove"]]
+    ck = oracle_for(FOUNDERS["schema"], tuples)
+    res = [ck.check(to_oracle_item(parse_check(s))) for s in FOUNDERS["checks"]]
+    assert all(p == ref.HAS for p, _ in res) == FOUNDERS["expected_all_negative"]
+
+
+def _suite(name):
+    return next(s for s in SEM["suites"] if s["name"] == name)
+
+
+S1 = _suite("gdocs-arrows-exclusion-intersection-wildcard")
+
+
+@pytest.mark.parametrize("chk", S1["checks"], ids=lambda c: c[0])
+def test_semantics_rewrites(chk):
+    ck = oracle_for(S1["schema"], S1["tuples"], now=iso_to_unix(SEM["now"]))
+    assert ck.check(to_oracle_item(parse_check(chk[0]))) == expected_code(chk[1])
+
+
+S2 = _suite("depth-budget")
+
+
+@pytest.mark.parametrize("chk", S2["depth_checks"], ids=lambda c: f"{c[0]}-d{c[1]}")
+def test_semantics_depth(chk):
+    ck = oracle_for(S2["schema"], S2["tuples"], max_depth=chk[1])
+    assert ck.check(to_oracle_item(parse_check(chk[0]))) == expected_code(chk[2])
+
+
+S3 = _suite("caveats-and-expiration")
+
+
+@pytest.mark.parametrize("chk", S3["caveat_checks"], ids=lambda c: f"{c[0]}-{c[1]}")
+def test_semantics_caveats(chk):
+    now = iso_to_unix(SEM["now"])
+    item = to_oracle_item(parse_check(chk[0]), chk[1])
+    dev = oracle_for(S3["schema"], S3["tuples"], now=now, evaluate_caveats=False)
+    assert dev.check(item) == expected_code(chk[2])
+    full = oracle_for(S3["schema"], S3["tuples"], now=now, evaluate_caveats=True)
+    assert full.check(item) == expected_code(chk[3])
+
+
+def test_schema_errors():
+    bad = [
+        "definition a { relation r: nosuch }",
+        "definition a { permission p = nosuch }",
+        "definition a { relation r: a }\ndefinition a {}",
+        "definition a { relation r: a  permission p = r->missing }",
+        "definition a { relation r: a:*  permission p = r->p }",
+        "definition a { relation r: a with nocaveat }",
+    ]
+    for s in bad:
+        with pytest.raises(ref.SchemaError):
+            ref.Schema(s)
+
+
+def test_precedence_and_flattening():
+    sc = ref.Schema("definition u {}\ndefinition d { relation a: u\nrelation b: u\nrelation c: u\n"
+                    "permission p = a + b - c\npermission q = a - b + c\npermission r = a & b + c }")
+    p = sc.relation("d", "p").expr
+    assert p.op == "exclude" and p.children[0].op == "union"
+    q = sc.relation("d", "q").expr
+    assert q.op == "exclude" and q.children[1].op == "union"
+    r = sc.relation("d", "r").expr
+    assert r.op == "intersect" and r.children[1].op == "union"
+
+
+def test_cel_partial_evaluation():
+    sc = ref.Schema('caveat c(a int, b string) { a > 3 || b == "x" }\ndefinition u {}')
+    e = sc.caveats["c"].expr
+    assert ref.cel_eval(e, {"a": 5}) is True
+    assert ref.cel_eval(e, {"a": 1}) is ref.UNKNOWN
+    assert ref.cel_eval(e, {"a": 1, "b": "y"}) is False
+    assert ref.cel_eval(e, {"b": "x"}) is True
+
+
+def test_cycle_is_max_depth_error():
+    # SpiceDB recursion on cyclic data that never reaches the subject ends in max depth
+    ck = oracle_for("definition user {}\ndefinition group { relation member: user | group#member }",
+                    ["group:a#member@group:b#member", "group:b#member@group:a#member",
+                     "group:b#member@user:x"], max_depth=50)
+    assert ck.check(to_oracle_item(parse_check("group:a#member@user:x"))) == (ref.HAS, 0)
+    assert ck.check(to_oracle_item(parse_check("group:a#member@user:y"))) == (0, ref.ITEM_ERR_MAX_DEPTH)
