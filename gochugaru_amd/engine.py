@@ -142,6 +142,14 @@ def load_library(path: str = _LIB_PATH):
         raise ImportError(
             f"libgck.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (make -C gochugaru_amd/csrc); the check engine has no CPU fallback")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7) and loads it by file name. If libgck were loaded first, the process
+    # would end up with two HIP runtimes and torch could not see the GPU. Loading torch first
+    # makes libgck's NEEDED libamdhip64.so.7 resolve to the already-loaded runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
