@@ -1,0 +1,202 @@
+"""bench.py — permission checks/sec at batch 64K on the 1B-tuple deep nested-group graph.
+
+Workload (BASELINE.json metric "permission checks/sec (whole node) at batch 64K, 1B tuples;
+HBM GB/s vs peak"; config 4 of BASELINE.json configs, replicated-graph mode, which fits one
+MI355X): tests/synth.py builds the seeded graph on every rank (identical, replicated), the
+engine ingests it through the C ABI (gck_load_csr), and each step is one 65,536-item
+``doc#view@user`` batch per GPU through ``gck_check_bulk_device`` with the items already
+resident in HBM. Ranks check independent batches (no collective on the data path), so
+scaling is weak: value = (checks of all ranks) / (max-over-ranks time).
+
+Also printed: the roofline of the dominant kernel (algorithmic bytes per launch / mean launch
+time, HIP events inside the timed region) and a CPU baseline (the C restatement oracle, all
+threads, on a bounded sample of the same batch, checked for 100 % agreement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+BATCH = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tuples", type=float, default=1e9, help="graph size (1e9 = BASELINE config)")
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")  # only timing barriers/reductions; no data-path collective
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from gochugaru_amd.engine import Engine
+    from tests import synth
+
+    t0 = time.time()
+    G = synth.build(args.tuples, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.time() - t0
+
+    t0 = time.time()
+    eng = Engine(device=local, profile=not args.no_profile)
+    eng.load_schema(synth.SCHEMA)
+    assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
+    assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW
+    eng.reserve_objects(synth.T_USER, G.n_users)
+    eng.reserve_objects(synth.T_GROUP, G.n_groups)
+    eng.reserve_objects(synth.T_DOC, G.n_docs)
+    eng.begin_snapshot(1)
+    keep = []
+    for rel, st, sr, n_rows, off, nbr in G.csrs():
+        off32 = off.to(torch.int32).contiguous()
+        nbr32 = nbr.contiguous()
+        keep.append((off32, nbr32))
+        eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr32.data_ptr(), nbr32.numel(), device=True)
+    torch.cuda.synchronize()
+    eng.commit_snapshot()
+    t_load = time.time() - t0
+    n_tuples = eng.tuple_count
+    dev_bytes = eng.device_bytes
+
+    items = synth.checks(G, args.batch, seed=1000 + rank)
+    perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
+    err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+
+    total_checks = world * args.batch * args.steps
+    value = total_checks / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    res = perm.cpu().numpy()
+    errs = err.cpu().numpy()
+
+    # ---- roofline of the dominant kernel (algorithmic bytes, SURVEY §8d / DESIGN.md) -------
+    n_batches = max(1, st["batches"])
+    alg_expand = st["row_lookups"] * 8 + st["membership_probes"] * 4          # k_expand reads
+    alg_edges = st["edges_enumerated"] * 4 + st["ext_edges"] * 12             # k_edges reads
+    alg_io = (20 + 1 + 4) * args.batch * n_batches                           # items in, results out
+    roof = None
+    if st["expand_launches"]:
+        kern = {
+            "k_expand": (alg_expand / st["expand_launches"], st["expand_ms"] / st["expand_launches"]),
+            "k_edges": (alg_edges / st["edges_launches"], st["edges_ms"] / st["edges_launches"]),
+        }
+        dom = max(kern, key=lambda k: kern[k][1])
+        b, ms = kern[dom]
+        achieved = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "alg_bytes_per_launch": int(b), "mean_launch_ms": round(ms, 5),
+                "launches_per_step": round(st["expand_launches"] / args.steps, 2),
+                "kernel_ms_share": {k: round(v[1] * st["expand_launches"] / max(1e-9, st["expand_ms"] + st["edges_ms"] + st["resolve_ms"]), 3) for k, v in kern.items()},
+                "batch_alg_GBs": round((alg_expand + alg_edges + alg_io) / elapsed / 1e9, 2)}
+
+    # ---- CPU baseline: the C restatement oracle on a bounded sample (rank 0, N=1) -----------
+    cpu = None
+    agree = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import corc
+        from oracle import spicedb_ref as ref
+
+        H = synth.host_arrays(G)
+        ids = corc.Ids(ref.Schema(synth.SCHEMA))
+        idx = {(synth.R_MEMBER, synth.T_USER, synth.ELLIPSIS, False): 0,
+               (synth.R_MEMBER, synth.T_GROUP, synth.R_MEMBER, False): 1,
+               (synth.R_VIEWER, synth.T_GROUP, synth.R_MEMBER, False): 2}
+        prog = corc.encode_program(ids, idx)
+        tab = corc.make_csr_table([(H["mem_user_off"], H["mem_user_nbr"], None, None, G.n_groups),
+                                   (H["mem_group_off"], H["mem_group_nbr"], None, None, G.n_groups),
+                                   (H["viewer_off"], H["viewer_nbr"], None, None, G.n_docs)])
+        host_items = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        # calibrate on a small prefix, then run a sample sized to the time budget
+        t0 = time.perf_counter()
+        corc.check(prog, tab, host_items[:1024], threads=threads)
+        per = (time.perf_counter() - t0) / 1024
+        n_s = int(min(len(host_items), max(1024, args.cpu_seconds / max(per, 1e-9))))
+        t0 = time.perf_counter()
+        cp, ce, _ = corc.check(prog, tab, host_items[:n_s], threads=threads)
+        dt = time.perf_counter() - t0
+        agree = float(np.mean((cp == res[:n_s]) & (ce == errs[:n_s])))
+        cpu = {"value": round(n_s / dt, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+               "sample": f"first {n_s} of the {args.batch}-check batch, same 1B-tuple graph, C oracle "
+                         f"(oracle/check_oracle.c, OpenMP {threads} threads), {dt:.1f}s"}
+
+    if rank == 0:
+        line = {
+            "metric": "permission checks/sec (whole node) at batch 64K, 1B tuples",
+            "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (tests/synth.py, seed 20251003): deep nested groups, 25 layers, Pareto(2.1) group sizes",
+            "config": {"workload": "config4-deep-nested-groups-replicated", "tuples": n_tuples,
+                       "batch_per_gpu": args.batch, "users": G.n_users, "groups": G.n_groups,
+                       "docs": G.n_docs, "parallelism": f"batch-sharded x{world}, graph replicated",
+                       "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
+            "roofline": roof, "cpu_baseline": cpu,
+            "oracle_agreement": agree,
+            "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),
+                           "COND": int((res == 3).sum()), "ERR": int((errs != 0).sum())},
+            "engine": {"levels_per_batch": round(st["levels"] / n_batches, 1),
+                       "entries_per_batch": int(st["entries_expanded"] / n_batches),
+                       "edges_per_batch": int(st["edges_enumerated"] / n_batches),
+                       "probes_per_batch": int(st["membership_probes"] / n_batches),
+                       "device_ms_per_batch": round(st["kernel_ms"], 3)},
+            "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,6 +69,7 @@ struct Workspace {
   int32_t* d_err = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // GCK_FLAG_PROFILE
   std::vector<void*> allocs;
 };
 
@@ -681,6 +682,8 @@ void device_free(Engine& e) {
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     if (w->ev2) (void)hipEventDestroy(w->ev2);
+    for (hipEvent_t ev : w->pev)
+      if (ev) (void)hipEventDestroy(ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     e.ws = nullptr;
@@ -803,6 +806,7 @@ static Workspace* ensure_workspace(Engine& e) {
     HIP_OK(hipEventCreate(&w->ev0));
     HIP_OK(hipEventCreate(&w->ev1));
     HIP_OK(hipEventCreate(&w->ev2));
+    for (hipEvent_t& ev : w->pev) HIP_OK(hipEventCreate(&ev));
   } catch (...) {
     free_list(w->allocs);
     if (w->h_ctr) (void)hipHostFree(w->h_ctr);
@@ -855,6 +859,7 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   hipLaunchKernelGGL(k_init, dim3(grid_n), dim3(kBlock), 0, st, c, d_items, n, w.fr[0], w.item_err);
   HIP_OK(hipGetLastError());
 
+  const bool profile = (e.cfg.flags & GCK_FLAG_PROFILE) != 0;
   uint32_t n_cur = n;
   int cur = 0;
   const uint32_t level_cap = 64 * c.max_depth + 64;
@@ -863,14 +868,29 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
     if (level > level_cap) throw Error(GCK_E_DEVICE, "level cap exceeded (engine invariant)");
     c.level = level;
     c.next = w.fr[cur ^ 1];
+    if (profile) HIP_OK(hipEventRecord(w.pev[0], st));
     hipLaunchKernelGGL(k_expand, dim3((n_cur + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c,
                        w.fr[cur], n_cur);
+    if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
     hipLaunchKernelGGL(k_edges, dim3(2048), dim3(kBlock), 0, st, c);
+    if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
     hipLaunchKernelGGL(k_resolve, dim3(1024), dim3(kBlock), 0, st, c);
+    if (profile) HIP_OK(hipEventRecord(w.pev[3], st));
     hipLaunchKernelGGL(k_level_end, dim3(1), dim3(1), 0, st, w.ctr);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    if (profile) {
+      float a = 0.f, b = 0.f, r = 0.f;
+      HIP_OK(hipEventElapsedTime(&a, w.pev[0], w.pev[1]));
+      HIP_OK(hipEventElapsedTime(&b, w.pev[1], w.pev[2]));
+      HIP_OK(hipEventElapsedTime(&r, w.pev[2], w.pev[3]));
+      e.stats.expand_ms += a;
+      e.stats.edges_ms += b;
+      e.stats.resolve_ms += r;
+      e.stats.expand_launches++;
+      e.stats.edges_launches++;
+    }
     if (w.h_ctr->overflow) return false;
     n_cur = w.h_ctr->last_next;
     cur ^= 1;

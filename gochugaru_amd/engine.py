@@ -44,6 +44,7 @@ REL_INVALID = 0xFFFE  # an id no schema relation has (never equal to ELLIPSIS)
 CONSISTENCY_MIN_LATENCY, CONSISTENCY_FULL, CONSISTENCY_AT_LEAST, CONSISTENCY_SNAPSHOT = 0, 1, 2, 3
 INTERN_CREATE = 1
 MEM_DEVICE = 1
+FLAG_PROFILE = 1
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -92,7 +93,9 @@ class _Stats(C.Structure):
                 ("row_lookups", C.c_uint64), ("membership_probes", C.c_uint64),
                 ("edges_enumerated", C.c_uint64), ("ext_edges", C.c_uint64),
                 ("queries", C.c_uint64), ("joins", C.c_uint64), ("retries", C.c_uint64),
-                ("kernel_ms", C.c_double), ("expand_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("expand_ms", C.c_double), ("edges_ms", C.c_double),
+                ("resolve_ms", C.c_double), ("expand_launches", C.c_uint64),
+                ("edges_launches", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -174,9 +177,10 @@ class Engine:
 
     def __init__(self, device: int = 0, max_depth: int = 50, max_batch: int = 65536,
                  visited_capacity: int = 0, frontier_capacity: int = 0,
-                 segment_capacity: int = 0, query_capacity: int = 0):
+                 segment_capacity: int = 0, query_capacity: int = 0, profile: bool = False):
         lib = load_library()
-        cfg = _Config(device, max_depth, max_batch, 0, visited_capacity, frontier_capacity,
+        cfg = _Config(device, max_depth, max_batch, FLAG_PROFILE if profile else 0,
+                      visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity)
         h = _P()
         _check(lib.gck_create(C.byref(cfg), C.byref(h)))

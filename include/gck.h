@@ -79,6 +79,7 @@ extern "C" {
 /* ---- flags ---------------------------------------------------------------------------- */
 #define GCK_INTERN_CREATE 1u     /* gck_intern: create ids for unseen strings */
 #define GCK_MEM_DEVICE 1u        /* gck_load_csr: pointers are device memory */
+#define GCK_FLAG_PROFILE 1u      /* gck_config.flags: time every kernel with HIP events */
 
 typedef struct gck_engine gck_engine;
 
@@ -86,7 +87,7 @@ typedef struct gck_config {
   int32_t device;              /* HIP device ordinal */
   uint32_t max_depth;          /* dispatch depth budget; 0 = 50 (SpiceDB default) */
   uint32_t max_batch;          /* checks per device launch sequence; 0 = 65536 */
-  uint32_t flags;              /* reserved, 0 */
+  uint32_t flags;              /* GCK_FLAG_* */
   uint64_t visited_capacity;   /* slots of the per-batch visited hash (power of 2); 0 = auto */
   uint64_t frontier_capacity;  /* entries per frontier buffer; 0 = auto */
   uint64_t segment_capacity;   /* row segments per level; 0 = auto */
@@ -133,8 +134,12 @@ typedef struct gck_stats {
   uint64_t queries;            /* queries allocated (checks + join operands) */
   uint64_t joins;              /* intersection/exclusion/all() joins spawned */
   uint64_t retries;            /* batch splits after a workspace overflow */
-  double kernel_ms;            /* device time of the last batch (HIP events) */
-  double expand_ms;            /* device time of the last batch's expand kernels */
+  double kernel_ms;            /* device time of the last gck_check_bulk* call (HIP events) */
+  double expand_ms;            /* GCK_FLAG_PROFILE: summed k_expand time (all batches) */
+  double edges_ms;             /* GCK_FLAG_PROFILE: summed k_edges time */
+  double resolve_ms;           /* GCK_FLAG_PROFILE: summed k_resolve time */
+  uint64_t expand_launches;    /* GCK_FLAG_PROFILE: k_expand launches timed */
+  uint64_t edges_launches;     /* GCK_FLAG_PROFILE: k_edges launches timed */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
