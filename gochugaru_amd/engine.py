@@ -45,6 +45,7 @@ CONSISTENCY_MIN_LATENCY, CONSISTENCY_FULL, CONSISTENCY_AT_LEAST, CONSISTENCY_SNA
 INTERN_CREATE = 1
 MEM_DEVICE = 1
 FLAG_PROFILE = 1
+FLAG_NO_BUNDLE = 2
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -81,7 +82,9 @@ class _Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_depth", C.c_uint32), ("max_batch", C.c_uint32),
                 ("flags", C.c_uint32), ("visited_capacity", C.c_uint64),
                 ("frontier_capacity", C.c_uint64), ("segment_capacity", C.c_uint64),
-                ("query_capacity", C.c_uint64)]
+                ("query_capacity", C.c_uint64), ("bundle_checks", C.c_uint32),
+                ("bundle_frontier", C.c_uint32), ("bundle_visited", C.c_uint32),
+                ("bundle_waves_per_cu", C.c_uint32)]
 
 
 class _Consistency(C.Structure):
@@ -95,7 +98,8 @@ class _Stats(C.Structure):
                 ("queries", C.c_uint64), ("joins", C.c_uint64), ("retries", C.c_uint64),
                 ("kernel_ms", C.c_double), ("expand_ms", C.c_double), ("edges_ms", C.c_double),
                 ("resolve_ms", C.c_double), ("expand_launches", C.c_uint64),
-                ("edges_launches", C.c_uint64)]
+                ("edges_launches", C.c_uint64), ("bundle_ms", C.c_double),
+                ("bundle_launches", C.c_uint64), ("deferred", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -177,11 +181,14 @@ class Engine:
 
     def __init__(self, device: int = 0, max_depth: int = 50, max_batch: int = 65536,
                  visited_capacity: int = 0, frontier_capacity: int = 0,
-                 segment_capacity: int = 0, query_capacity: int = 0, profile: bool = False):
+                 segment_capacity: int = 0, query_capacity: int = 0, profile: bool = False,
+                 wide_only: bool = False, bundle_checks: int = 0, bundle_frontier: int = 0,
+                 bundle_visited: int = 0, bundle_waves_per_cu: int = 0):
         lib = load_library()
-        cfg = _Config(device, max_depth, max_batch, FLAG_PROFILE if profile else 0,
-                      visited_capacity, frontier_capacity,
-                      segment_capacity, query_capacity)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
+        cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
+                      segment_capacity, query_capacity, bundle_checks, bundle_frontier,
+                      bundle_visited, bundle_waves_per_cu)
         h = _P()
         _check(lib.gck_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -80,6 +80,7 @@ extern "C" {
 #define GCK_INTERN_CREATE 1u     /* gck_intern: create ids for unseen strings */
 #define GCK_MEM_DEVICE 1u        /* gck_load_csr: pointers are device memory */
 #define GCK_FLAG_PROFILE 1u      /* gck_config.flags: time every kernel with HIP events */
+#define GCK_FLAG_NO_BUNDLE 2u    /* gck_config.flags: grid-wide level-synchronous path only */
 
 typedef struct gck_engine gck_engine;
 
@@ -92,6 +93,10 @@ typedef struct gck_config {
   uint64_t frontier_capacity;  /* entries per frontier buffer; 0 = auto */
   uint64_t segment_capacity;   /* row segments per level; 0 = auto */
   uint64_t query_capacity;     /* queries per batch (checks + sub-queries of joins); 0 = auto */
+  uint32_t bundle_checks;      /* checks per wavefront bundle (1..64); 0 = 16 */
+  uint32_t bundle_frontier;    /* frontier entries per wavefront; 0 = 4096 */
+  uint32_t bundle_visited;     /* visited slots per wavefront (power of 2); 0 = 8192 */
+  uint32_t bundle_waves_per_cu;/* resident wavefronts per CU for the bundle kernel; 0 = 16 */
 } gck_config;
 
 /* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
@@ -140,6 +145,9 @@ typedef struct gck_stats {
   double resolve_ms;           /* GCK_FLAG_PROFILE: summed k_resolve time */
   uint64_t expand_launches;    /* GCK_FLAG_PROFILE: k_expand launches timed */
   uint64_t edges_launches;     /* GCK_FLAG_PROFILE: k_edges launches timed */
+  double bundle_ms;            /* GCK_FLAG_PROFILE: summed k_bundles time */
+  uint64_t bundle_launches;    /* GCK_FLAG_PROFILE: k_bundles launches timed */
+  uint64_t deferred;           /* checks re-run by the grid-wide path after a bundle overflow */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

@@ -147,17 +147,47 @@ def test_semantics_caveats_device_contract():
 
 # ---- random graphs vs the oracle -------------------------------------------------------------
 
+PATHS = {
+    # persistent wave-bundle kernel (default)
+    "bundle": {},
+    # grid-wide level-synchronous kernels only
+    "wide": {"wide_only": True},
+    # tiny per-wave scratch: most bundles overflow and are re-run by the grid-wide path
+    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 16},
+    # one check per wavefront, few resident waves
+    "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4},
+}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("family", sorted(gen.FAMILIES))
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_random_parity(family, seed):
+def test_random_parity(family, seed, path):
     schema, tuples, checks = gen.FAMILIES[family](seed)
     ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6, evaluate_caveats=False)
     want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
-    e = make_engine(schema, tuples)
+    e = make_engine(schema, tuples, **PATHS[path])
     got = device_results(e, checks, now_us=gen.NOW_US)
     bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
     assert not bad, bad[:10]
+    if path == "bundle-deferred":
+        assert e.stats()["deferred"] > 0
+    if path == "bundle":
+        assert e.stats()["deferred"] == 0
     e.close()
+
+
+@pytest.mark.parametrize("path", ["bundle", "wide"])
+def test_semantics_all_paths(path):
+    for s in SEM["suites"]:
+        rows = s.get("checks") or s.get("caveat_checks")
+        if not rows:
+            continue
+        e = make_engine(s["schema"], s["tuples"], **PATHS[path])
+        got = device_results(e, [c[0] for c in rows])
+        col = 1 if "checks" in s else 2
+        assert got == [expected_code(c[col]) for c in rows], s["name"]
+        e.close()
 
 
 def test_small_batches_and_overflow_retry():
@@ -166,11 +196,17 @@ def test_small_batches_and_overflow_retry():
     want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
     # tiny workspace: forces batch splits and overflow retries, results must not change
     e = make_engine(schema, tuples, max_batch=37, frontier_capacity=64, segment_capacity=64,
-                    visited_capacity=256, query_capacity=64)
+                    visited_capacity=256, query_capacity=64, wide_only=True)
     got = device_results(e, checks, now_us=gen.NOW_US)
     assert got == want
     st = e.stats()
     assert st["batches"] >= len(checks) // 37
+    e.close()
+    # the same through bundles whose deferrals land in the tiny wide workspace
+    e = make_engine(schema, tuples, max_batch=37, frontier_capacity=64, segment_capacity=64,
+                    visited_capacity=256, query_capacity=64, bundle_checks=2, bundle_frontier=4,
+                    bundle_visited=8)
+    assert device_results(e, checks, now_us=gen.NOW_US) == want
     e.close()
 
 

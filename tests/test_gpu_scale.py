@@ -55,8 +55,13 @@ def test_config4_shape_vs_c_oracle():
     e2 = load_engine(G, max_batch=10007)
     p2, e2r = run(e2, items[:50000])
     assert np.array_equal(p2, perm[:50000]) and np.array_equal(e2r, err[:50000])
+    # the grid-wide path gives the same answers
+    e3 = load_engine(G, wide_only=True)
+    p3, e3r = run(e3, items)
+    assert np.array_equal(p3, perm) and np.array_equal(e3r, err)
     e.close()
     e2.close()
+    e3.close()
 
 
 def test_positive_half_at_scale():
