@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -684,6 +686,13 @@ struct LJoin {
   uint32_t pad;
 };
 
+// LDS words that other lanes of the wave update concurrently: always re-load (a plain load may
+// be reused by the compiler across a sibling lane's atomics).
+template <class T>
+__device__ __forceinline__ T lds_ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 struct WaveLDS {
   LQuery q[kBQ];
   LJoin j[kBJ];
@@ -708,6 +717,7 @@ struct BundleArgs {
   Entry* fr_base;
   unsigned long long* vis_base;
   uint32_t* slot_epoch;
+  uint32_t* dbg;  // GCK_DEBUG_BUNDLE: bundle 0's tables are dumped here
 };
 
 struct BCtx {
@@ -872,7 +882,7 @@ __device__ void b_spawn(const Ctx& c, const BCtx& b, uint32_t q, uint32_t obj, u
 // decision resolved a join, i.e. its parent may now be decidable.
 __device__ bool b_finalize(WaveLDS* L, uint32_t qi, uint32_t res) {
   LQuery* q = &L->q[qi];
-  uint32_t f = q->flags;
+  uint32_t f = lds_ld(&q->flags);
   for (;;) {
     if (f & QF_DONE) return false;
     uint32_t prev = atomicCAS(&q->flags, f, f | QF_DONE | (res << QF_RES_SHIFT));
@@ -979,7 +989,7 @@ __device__ void b_distribute(const Ctx& c, const BCtx& b, int lane, uint32_t csr
         ok = visible(r, p, c.now_us);
         cnd |= (r.cav[p] != 0);
       }
-      if (ok && x != kWildcard && !(L->q[sq & 0x7FFFFFFFu].flags & QF_DONE))
+      if (ok && x != kWildcard && !(lds_ld(&L->q[sq & 0x7FFFFFFFu].flags) & QF_DONE))
         b_push(b, sq & 0x7FFFFFFFu, x, (uint16_t)(st & 0xFFFF), st >> 16, cnd);
     }
   }
@@ -1093,7 +1103,7 @@ __global__ void __launch_bounds__(kBlock) k_bundles(Ctx c, BundleArgs a) {
         DevCheck s{};
         if (act) {
           e = cur[i];
-          act = !(L->q[e.q].flags & QF_DONE);
+          act = !(lds_ld(&L->q[e.q].flags) & QF_DONE);
         }
         if (act) {
           ++s_exp;
@@ -1191,21 +1201,25 @@ __global__ void __launch_bounds__(kBlock) k_bundles(Ctx c, BundleArgs a) {
         s_rows += rows;
         s_probes += probes;
       }
-      // resolve: decide queries, cascade through joins until stable
+      // resolve: decide queries, cascade through joins until stable. Not after an overflow:
+      // a dropped push would read as "no live entries" and decide a query too early.
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
+      if (L->overflow) break;
       for (int iter = 0; iter < kBQ + 2; ++iter) {
         const uint32_t qn = min(L->q_count, (uint32_t)kBQ);
         bool changed = false;
         for (uint32_t qb = 0; qb < qn; qb += 64) {
           const uint32_t qi = qb + lane;
           if (qi < qn) {
-            const uint32_t f = L->q[qi].flags;
+            const uint32_t f = lds_ld(&L->q[qi].flags);
             if (!(f & QF_DONE)) {
               if (f & QF_FOUND_Y) {
                 changed |= b_finalize(L, qi, GCK_PERM_HAS);
-              } else if (L->q[qi].last_alive <= level && L->q[qi].pending == 0) {
-                changed |= b_finalize(L, qi, result_from_flags(f));
+              } else if (lds_ld(&L->q[qi].last_alive) <= level && lds_ld(&L->q[qi].pending) == 0) {
+                // re-read: a sibling lane may have resolved this query's last join (its
+                // contribution is written before the pending decrement we just observed)
+                changed |= b_finalize(L, qi, result_from_flags(lds_ld(&L->q[qi].flags)));
               }
             }
           }
@@ -1222,6 +1236,20 @@ __global__ void __launch_bounds__(kBlock) k_bundles(Ctx c, BundleArgs a) {
       Entry* t = cur;
       cur = nxt;
       nxt = t;
+    }
+    if (a.dbg && bi == 0) {  // debug dump of bundle 0's final query/join tables
+      const uint32_t qn = min(L->q_count, (uint32_t)kBQ), jn = min(L->j_count, (uint32_t)kBJ);
+      for (uint32_t k = lane; k < qn; k += 64) {
+        uint32_t* d = a.dbg + 4 + k * 6;
+        d[0] = L->q[k].flags; d[1] = (uint32_t)L->q[k].pending; d[2] = L->q[k].last_alive;
+        d[3] = L->q[k].parent_join; d[4] = L->q[k].operand; d[5] = L->q[k].check;
+      }
+      for (uint32_t k = lane; k < jn; k += 64) {
+        uint32_t* d = a.dbg + 4 + kBQ * 6 + k * 8;
+        d[0] = L->j[k].parent_q; d[1] = L->j[k].first_child; d[2] = L->j[k].n_ops; d[3] = L->j[k].op;
+        d[4] = L->j[k].cond; d[5] = L->j[k].state; d[6] = (uint32_t)L->j[k].remaining;
+      }
+      if (lane == 0) { a.dbg[0] = qn; a.dbg[1] = jn; a.dbg[2] = L->overflow; a.dbg[3] = epoch; }
     }
     // outputs (undecided checks after an overflow are deferred to the grid-wide path)
     const bool ovf = L->overflow != 0;
@@ -1618,6 +1646,11 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   a.fr_base = w.b_fr;
   a.vis_base = w.b_vis;
   a.slot_epoch = w.b_epoch;
+  static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
+  static uint32_t* dbg = nullptr;
+  const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;
+  if (dbg_on && !dbg) HIP_OK(hipMalloc(&dbg, dbg_words * 4));
+  a.dbg = dbg_on ? dbg : nullptr;
   HIP_OK(hipEventRecord(w.ev0, st));
   HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
   HIP_OK(hipMemsetAsync(w.b_ctrs, 0, 4 * sizeof(unsigned), st));
@@ -1646,6 +1679,21 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   e.stats.ext_edges += h.ext_edges;
   e.stats.queries += n;
   e.stats.batches++;
+  if (dbg_on) {
+    std::vector<uint32_t> h(dbg_words);
+    HIP_OK(hipMemcpy(h.data(), dbg, dbg_words * 4, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[gck bundle0] queries=%u joins=%u overflow=%u epoch=%u\n", h[0], h[1], h[2], h[3]);
+    for (uint32_t k = 0; k < h[0] && k < (uint32_t)kBQ; ++k) {
+      const uint32_t* d = h.data() + 4 + k * 6;
+      fprintf(stderr, "  q%-3u flags=%#x res=%u pending=%d last_alive=%u parent_join=%d operand=%u check=%u\n", k,
+              d[0], (d[0] >> 8) & 0xF, (int)d[1], d[2], (int)d[3], d[4], d[5]);
+    }
+    for (uint32_t k = 0; k < h[1] && k < (uint32_t)kBJ; ++k) {
+      const uint32_t* d = h.data() + 4 + kBQ * 6 + k * 8;
+      fprintf(stderr, "  j%-3u parent=%u first=%u n=%u op=%u cond=%u state=%#x remaining=%d\n", k, d[0], d[1],
+              d[2], d[3], d[4], d[5], (int)d[6]);
+    }
+  }
   const uint32_t n_def = w.h_bctrs[1];
   if (n_def > n) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
   if (n_def == 0) return;

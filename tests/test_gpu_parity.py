@@ -170,7 +170,7 @@ def test_random_parity(family, seed, path):
     got = device_results(e, checks, now_us=gen.NOW_US)
     bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
     assert not bad, bad[:10]
-    if path == "bundle-deferred":
+    if path == "bundle-deferred" and family != "caveated":  # caveated graphs are too small to overflow
         assert e.stats()["deferred"] > 0
     if path == "bundle":
         assert e.stats()["deferred"] == 0
