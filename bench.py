@@ -38,6 +38,13 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--bundle-checks", type=int, default=0)
+    ap.add_argument("--bundle-frontier", type=int, default=0)
+    ap.add_argument("--bundle-visited", type=int, default=0)
+    ap.add_argument("--bundle-waves", type=int, default=0)
+    ap.add_argument("--bundle-budget", type=int, default=0)
+    ap.add_argument("--giant-slots", type=int, default=0)
+    ap.add_argument("--wide-only", action="store_true")
     return ap.parse_args()
 
 
@@ -64,7 +71,10 @@ def main():
     t_gen = time.time() - t0
 
     t0 = time.time()
-    eng = Engine(device=local, profile=not args.no_profile)
+    eng = Engine(device=local, profile=not args.no_profile, wide_only=args.wide_only,
+                 bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
+                 bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
+                 bundle_budget=args.bundle_budget, giant_slots=args.giant_slots)
     eng.load_schema(synth.SCHEMA)
     assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
     assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW
@@ -189,7 +199,11 @@ def main():
                        "entries_per_batch": int(st["entries_expanded"] / n_batches),
                        "edges_per_batch": int(st["edges_enumerated"] / n_batches),
                        "probes_per_batch": int(st["membership_probes"] / n_batches),
-                       "device_ms_per_batch": round(st["kernel_ms"], 3)},
+                       "device_ms_per_batch": round(st["kernel_ms"], 3),
+                       "bundle_ms_per_batch": round(st["bundle_ms"] / n_batches, 4),
+                       "deferred_per_batch": round(st["deferred"] / n_batches, 1),
+                       "giant_ms_per_batch": round(st["giant_ms"] / n_batches, 4),
+                       "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
         }
         print(json.dumps(line), flush=True)

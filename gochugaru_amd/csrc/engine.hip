@@ -73,13 +73,20 @@ struct Workspace {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // GCK_FLAG_PROFILE
   // bundle path
-  uint32_t b_checks = 16, b_fc = 4096, b_vslots = 8192, b_blocks = 0;
+  uint32_t b_checks = 16, b_fc = 4096, b_vslots = 16384, b_blocks = 0;
   Entry* b_fr = nullptr;
   unsigned long long* b_vis = nullptr;
-  uint32_t* b_epoch = nullptr;
+  uint32_t* b_vlog = nullptr;  // per slot: claimed visited slots (cleared by the bundle)
   uint32_t* b_deferred = nullptr;
-  unsigned* b_ctrs = nullptr;      // [0] bundle counter, [1] deferred count
+  unsigned* b_ctrs = nullptr;      // [0] bundle ctr, [1] deferred, [2] giant bundle ctr, [3] deferred2
   unsigned* h_bctrs = nullptr;     // pinned
+  uint32_t b_budget = 1024;
+  // giant-check stage: one 16-wave workgroup per bundle
+  uint32_t g_fc = 65536, g_vslots = 262144, g_slots = 0;
+  Entry* g_fr = nullptr;
+  unsigned long long* g_vis = nullptr;
+  uint32_t* g_vlog = nullptr;
+  uint32_t* g_deferred = nullptr;
   gck_item* def_items = nullptr;
   uint8_t* def_perm = nullptr;
   int32_t* def_err = nullptr;
@@ -201,6 +208,47 @@ __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t n
   if (!r.is_ext) return true;
   int64_t x = r.exp_us[pos];
   return x == 0 || x > now_us;
+}
+
+// Is (obj, sid) in the membership index? One dependent line in the common case.
+__device__ __forceinline__ bool hash_member(const DevCSR& r, uint32_t obj, uint32_t sid, uint32_t& probes) {
+  const unsigned long long key = ((unsigned long long)obj << 32) | sid;
+  unsigned long long h = mix64(key) & r.mmask;
+  for (;;) {
+    ++probes;
+    const unsigned long long v = r.mhash[h];
+    if (v == key) return true;
+    if (v == kEmptyKey) return false;
+    h = (h + 1) & r.mmask;
+  }
+}
+
+// checkDirect membership on one CSR: the subject itself (`direct`) and/or the wildcard
+// (`wild`). Returns 0 = absent, 1 = present, 2 = present through a caveated edge.
+__device__ __forceinline__ uint32_t member_test(const DevCSR& r, uint32_t obj, uint32_t sid, bool direct,
+                                                bool wild, int64_t now_us, uint32_t& rows,
+                                                uint32_t& probes) {
+  if (obj >= r.n_rows) return 0;
+  if (r.mhash) {  // plain direct CSR: hashed index, no row read
+    if (direct && hash_member(r, obj, sid, probes)) return 1;
+    if (wild && hash_member(r, obj, kWildcard, probes)) return 1;
+    return 0;
+  }
+  ++rows;
+  uint32_t best = 0;
+  if (direct) {
+    const uint32_t p = row_find(r, obj, sid, probes);
+    if (p != kNone && visible(r, p, now_us)) best = (r.is_ext && r.cav[p] != 0) ? 2u : 1u;
+  }
+  if (wild && best != 1) {
+    const uint32_t b = r.off[obj], en = r.off[obj + 1];
+    ++probes;
+    if (en > b && r.nbr[en - 1] == kWildcard && visible(r, en - 1, now_us)) {
+      const uint32_t m = (r.is_ext && r.cav[en - 1] != 0) ? 2u : 1u;
+      if (best == 0 || m == 1) best = m;
+    }
+  }
+  return best;
 }
 
 __device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_t obj, uint32_t q,
@@ -409,25 +457,11 @@ __global__ void __launch_bounds__(kBlock) k_expand(Ctx c, const Entry* __restric
               for (int pass = 0; pass < 2 && !done; ++pass) {
                 uint32_t ci = pass ? it.csr_ext : it.csr_plain;
                 if (ci == kNone) continue;
-                const DevCSR& r = c.csrs[ci];
-                if (e.obj >= r.n_rows) continue;
-                ++rows;
-                if (direct) {
-                  uint32_t p = row_find(r, e.obj, s.sid, probes);
-                  if (p != kNone && visible(r, p, c.now_us)) {
-                    uint32_t cond = e.cond | (r.is_ext ? (r.cav[p] != 0) : 0u);
-                    set_found(c, e.q, cond);
-                    if (!cond) done = true;
-                  }
-                }
-                if (wild && !done) {
-                  uint32_t b = r.off[e.obj], en = r.off[e.obj + 1];
-                  ++probes;
-                  if (en > b && r.nbr[en - 1] == kWildcard && visible(r, en - 1, c.now_us)) {
-                    uint32_t cond = e.cond | (r.is_ext ? (r.cav[en - 1] != 0) : 0u);
-                    set_found(c, e.q, cond);
-                    if (!cond) done = true;
-                  }
+                const uint32_t m = member_test(c.csrs[ci], e.obj, s.sid, direct, wild, c.now_us, rows, probes);
+                if (m) {
+                  const uint32_t cond = e.cond | (m == 2);
+                  set_found(c, e.q, cond);
+                  if (!cond) done = true;
                 }
               }
             }
@@ -646,635 +680,46 @@ __global__ void __launch_bounds__(kBlock) k_final(const DevQuery* __restrict__ q
   out_err[i] = err;
 }
 
-// =============================================================================================
-// Bundle path: one persistent launch; each wavefront owns a bundle of B checks and runs their
-// level-synchronous BFS to completion without any grid-wide synchronisation.
-//   * the bundle's queries/joins/subjects live in LDS (per wave);
-//   * frontiers live in a per-wave global scratch ring (L2/MALL-resident), appended with an
-//     LDS atomic counter;
-//   * the visited set is a per-wave, epoch-tagged open-addressing table in global memory
-//     (no per-batch clearing: a slot from an older epoch is free);
-//   * userset/arrow rows are enumerated wave-cooperatively: lanes publish (row, len) into LDS,
-//     a 64-lane prefix sum assigns edges to lanes, so one long row is read by all 64 lanes
-//     with coalesced loads;
-//   * a bundle that outgrows its scratch (frontier, queries, joins, visited probes) is
-//     deferred: its undecided checks are re-run by the grid-wide level-synchronous path.
-// Levels inside a bundle are synchronous, so first visits happen at minimal depth exactly as in
-// the grid-wide path and the results are identical (tests/test_gpu_parity.py forces both).
-// =============================================================================================
-
 constexpr int kWaves = kBlock / 64;
-constexpr int kBQ = 128;      // queries per bundle (checks + join operands)
-constexpr int kBJ = 32;       // joins per bundle
-constexpr int kBMax = 64;     // max checks per bundle
-constexpr uint32_t kEpochShift = 53;
-constexpr uint32_t kEpochMax = 2047;
-constexpr uint32_t kNoJoin = 0xFFFFFFFFu;
 
-struct LQuery {
-  uint32_t flags;
-  int32_t pending;
-  uint32_t last_alive;
-  uint32_t parent_join;  // kNoJoin for a bundle check
-  uint32_t operand;
-  uint32_t check;        // local check index (subject)
-};
+#include "bundle.inc"
 
-struct LJoin {
-  uint32_t parent_q, first_child, n_ops, op, cond, state;
-  int32_t remaining;
-  uint32_t pad;
-};
-
-// LDS words that other lanes of the wave update concurrently: always re-load (a plain load may
-// be reused by the compiler across a sibling lane's atomics).
-template <class T>
-__device__ __forceinline__ T lds_ld(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-struct WaveLDS {
-  LQuery q[kBQ];
-  LJoin j[kBJ];
-  DevCheck chk[kBMax];
-  int32_t err[kBMax];
-  // edge-distribution staging (one slot per lane)
-  uint32_t s_excl[64], s_begin[64], s_csr[64], s_q[64], s_tgt[64];
-  uint32_t next_n, q_count, j_count, overflow;
-};
-
-struct BundleArgs {
-  const gck_item* items;
-  uint32_t n;
-  uint8_t* out_perm;
-  int32_t* out_err;
-  uint32_t* deferred;
-  unsigned* n_deferred;
-  unsigned* bundle_ctr;
-  uint32_t B;
-  uint32_t FC;
-  uint32_t vmask;
-  Entry* fr_base;
-  unsigned long long* vis_base;
-  uint32_t* slot_epoch;
-  uint32_t* dbg;  // GCK_DEBUG_BUNDLE: bundle 0's tables are dumped here
-};
-
-struct BCtx {
-  WaveLDS* L;
-  Entry* next;
-  unsigned long long* V;
-  uint32_t vmask, FC, epoch, level;
-  uint32_t node_shift;  // key = epoch<<53 | q<<45 | node<<33 | cond<<32 | obj
-};
-
-__device__ __forceinline__ unsigned long long b_key(const BCtx& b, uint32_t q, uint32_t node,
-                                                    uint32_t cond, uint32_t obj) {
-  return ((unsigned long long)b.epoch << kEpochShift) | ((unsigned long long)q << 45) |
-         ((unsigned long long)node << 33) | ((unsigned long long)(cond & 1u) << 32) | obj;
-}
-
-__device__ __forceinline__ bool b_current(const BCtx& b, unsigned long long v) {
-  return (uint32_t)(v >> kEpochShift) == b.epoch;
-}
-
-__device__ bool b_vlookup(const BCtx& b, unsigned long long key) {
-  uint32_t h = (uint32_t)mix64(key) & b.vmask;
-  for (int p = 0; p < 64; ++p) {
-    unsigned long long v = __hip_atomic_load(&b.V[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!b_current(b, v)) return false;
-    if (v == key) return true;
-    h = (h + 1) & b.vmask;
-  }
-  return false;
-}
-
-// 1 inserted, 0 present, -1 table too full
-__device__ int b_vinsert(const BCtx& b, unsigned long long key) {
-  uint32_t h = (uint32_t)mix64(key) & b.vmask;
-  int probes = 0;
-  for (int it = 0; it < 256; ++it) {
-    unsigned long long v = __hip_atomic_load(&b.V[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (b_current(b, v)) {
-      if (v == key) return 0;
-      if (++probes >= 32) return -1;
-      h = (h + 1) & b.vmask;
-      continue;
+// Membership index build: one lane per edge of a plain direct-subject CSR. Each block owns 256
+// consecutive edges; two lanes find the block's first and last rows, then every lane finds its
+// row in that (usually 1-2 row) window.
+__global__ void __launch_bounds__(kBlock) k_build_mhash(const uint32_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ nbr, uint32_t n_rows,
+                                                        unsigned long long n_edges,
+                                                        unsigned long long* __restrict__ tab,
+                                                        unsigned long long mask) {
+  __shared__ uint32_t rows[2];
+  const unsigned long long e0 = (unsigned long long)blockIdx.x * kBlock;
+  if (threadIdx.x < 2) {
+    const unsigned long long t = threadIdx.x == 0 ? e0 : min(e0 + kBlock, n_edges) - 1;
+    uint32_t lo = 0, hi = n_rows;  // last row r with off[r] <= t
+    while (lo < hi) {
+      uint32_t mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= t) lo = mid;
+      else hi = mid - 1;
     }
-    unsigned long long prev = atomicCAS(&b.V[h], v, key);
-    if (prev == v) return 1;
-    if (prev == key) return 0;
-    if (b_current(b, prev)) {  // lost the slot to another key of this epoch
-      if (++probes >= 32) return -1;
-      h = (h + 1) & b.vmask;
-    }
+    rows[threadIdx.x] = lo;
   }
-  return -1;
-}
-
-__device__ __forceinline__ void b_push(const BCtx& b, uint32_t q, uint32_t obj, uint16_t node,
-                                       uint32_t depth, uint32_t cond) {
-  WaveLDS* L = b.L;
-  if (cond && b_vlookup(b, b_key(b, q, node, 0, obj))) return;
-  int r = b_vinsert(b, b_key(b, q, node, cond, obj));
-  if (r < 0) {
-    L->overflow = 1;
-    return;
+  __syncthreads();
+  const unsigned long long e = e0 + threadIdx.x;
+  if (e >= n_edges) return;
+  uint32_t lo = rows[0], hi = rows[1];
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= e) lo = mid;
+    else hi = mid - 1;
   }
-  if (r == 0) return;
-  uint32_t pos = atomicAdd(&L->next_n, 1u);
-  if (pos >= b.FC) {
-    L->overflow = 1;
-    return;
-  }
-  Entry e;
-  e.q = q;
-  e.obj = obj;
-  e.node = node;
-  e.depth = (uint8_t)(depth > 255 ? 255 : depth);
-  e.cond = (uint8_t)cond;
-  b.next[pos] = e;
-  L->q[q].last_alive = b.level + 1;
-}
-
-__device__ void b_spawn(const Ctx& c, const BCtx& b, uint32_t q, uint32_t obj, uint16_t node,
-                        uint32_t depth, uint32_t cond, uint32_t& rows) {
-  WaveLDS* L = b.L;
-  const DevNode nd = c.nodes[node];
-  uint32_t n_ops = 0;
-  if (nd.kind == NK_ARROW_ALL) {
-    bool missing = false;
-    for (uint32_t k = 0; k < nd.count; ++k) {
-      const DevItem it = c.items[nd.first + k];
-      for (int pass = 0; pass < 2; ++pass) {
-        uint32_t ci = pass ? it.csr_ext : it.csr_plain;
-        if (ci == kNone) continue;
-        const DevCSR& r = c.csrs[ci];
-        if (obj >= r.n_rows) continue;
-        ++rows;
-        for (uint32_t p = r.off[obj], e = r.off[obj + 1]; p < e; ++p) {
-          if (!visible(r, p, c.now_us)) continue;
-          if (it.target == kNoNode) missing = true;
-          ++n_ops;
-        }
-      }
-    }
-    if (n_ops == 0 || missing) return;
-  } else if (nd.kind == NK_NIL) {
-    return;
-  } else {
-    n_ops = nd.count;
-  }
-  uint32_t j = atomicAdd(&L->j_count, 1u);
-  uint32_t q0 = atomicAdd(&L->q_count, n_ops);
-  if (j >= (uint32_t)kBJ || q0 + n_ops > (uint32_t)kBQ) {
-    L->overflow = 1;
-    return;
-  }
-  LJoin J;
-  J.parent_q = q;
-  J.first_child = q0;
-  J.n_ops = n_ops;
-  J.op = nd.kind;
-  J.cond = cond;
-  J.state = 0;
-  J.remaining = (int32_t)n_ops;
-  J.pad = 0;
-  L->j[j] = J;
-  const uint32_t check = L->q[q].check;
-  for (uint32_t k = 0; k < n_ops; ++k) {
-    LQuery cq;
-    cq.flags = 0;
-    cq.pending = 0;
-    cq.last_alive = b.level;
-    cq.parent_join = j;
-    cq.operand = k;
-    cq.check = check;
-    L->q[q0 + k] = cq;
-  }
-  atomicAdd(&L->q[q].pending, 1);
-  if (nd.kind == NK_ARROW_ALL) {
-    uint32_t k = 0;
-    for (uint32_t t = 0; t < nd.count; ++t) {
-      const DevItem it = c.items[nd.first + t];
-      for (int pass = 0; pass < 2; ++pass) {
-        uint32_t ci = pass ? it.csr_ext : it.csr_plain;
-        if (ci == kNone) continue;
-        const DevCSR& r = c.csrs[ci];
-        if (obj >= r.n_rows) continue;
-        for (uint32_t p = r.off[obj], e = r.off[obj + 1]; p < e; ++p) {
-          if (!visible(r, p, c.now_us)) continue;
-          uint32_t cav = r.is_ext ? (r.cav[p] != 0) : 0u;
-          b_push(b, q0 + k, r.nbr[p], it.target, depth + 1, cav);
-          ++k;
-        }
-      }
-    }
-  } else {
-    for (uint32_t k = 0; k < n_ops; ++k) {
-      const DevItem it = c.items[nd.first + k];
-      b_push(b, q0 + k, obj, it.target, depth + it.dispatch, 0u);
-    }
-  }
-}
-
-// Decide one query of the bundle (no cascade: the caller iterates). Returns true when the
-// decision resolved a join, i.e. its parent may now be decidable.
-__device__ bool b_finalize(WaveLDS* L, uint32_t qi, uint32_t res) {
-  LQuery* q = &L->q[qi];
-  uint32_t f = lds_ld(&q->flags);
+  const unsigned long long key = ((unsigned long long)lo << 32) | nbr[e];
+  unsigned long long h = mix64(key) & mask;
   for (;;) {
-    if (f & QF_DONE) return false;
-    uint32_t prev = atomicCAS(&q->flags, f, f | QF_DONE | (res << QF_RES_SHIFT));
-    if (prev == f) break;
-    f = prev;
+    const unsigned long long prev = atomicCAS(&tab[h], kEmptyKey, key);
+    if (prev == kEmptyKey || prev == key) return;
+    h = (h + 1) & mask;
   }
-  const uint32_t j = q->parent_join;
-  if (j == kNoJoin) return false;
-  LJoin* J = &L->j[j];
-  const uint32_t op = J->op;
-  uint32_t bit;
-  bool early;
-  if (op == NK_EXCLUDE && q->operand == 0) {
-    bit = res == GCK_PERM_HAS ? JS_BASE_Y : res == GCK_PERM_NO ? JS_BASE_N
-          : res == GCK_PERM_CONDITIONAL ? JS_BASE_C : JS_BASE_ERR;
-    early = res == GCK_PERM_NO;
-  } else {
-    bit = res == GCK_PERM_HAS ? JS_ANY_Y : res == GCK_PERM_NO ? JS_ANY_N
-          : res == GCK_PERM_CONDITIONAL ? JS_ANY_C : JS_ANY_ERR;
-    early = (op == NK_EXCLUDE) ? res == GCK_PERM_HAS : res == GCK_PERM_NO;
-  }
-  atomicOr(&J->state, bit);
-  int rem = atomicSub(&J->remaining, 1) - 1;
-  if (!(rem == 0 || early)) return false;
-  uint32_t st = atomicOr(&J->state, (uint32_t)JS_RESOLVED);
-  if (st & JS_RESOLVED) return false;
-  uint32_t jr;
-  if (early) {
-    jr = GCK_PERM_NO;
-  } else if (op == NK_EXCLUDE) {
-    jr = (st & (JS_BASE_N | JS_ANY_Y)) ? GCK_PERM_NO
-         : (st & (JS_BASE_ERR | JS_ANY_ERR)) ? kResErr
-         : (st & (JS_BASE_C | JS_ANY_C)) ? GCK_PERM_CONDITIONAL : GCK_PERM_HAS;
-  } else {
-    jr = (st & JS_ANY_N) ? GCK_PERM_NO : (st & JS_ANY_ERR) ? kResErr
-         : (st & JS_ANY_C) ? GCK_PERM_CONDITIONAL : GCK_PERM_HAS;
-  }
-  if (rem > 0) {
-    for (uint32_t k = 0; k < J->n_ops; ++k) atomicOr(&L->q[J->first_child + k].flags, (uint32_t)(QF_DONE | QF_CANCELLED));
-  }
-  if (J->cond && jr == GCK_PERM_HAS) jr = GCK_PERM_CONDITIONAL;
-  LQuery* P = &L->q[J->parent_q];
-  uint32_t fbit = jr == GCK_PERM_HAS ? QF_FOUND_Y : jr == GCK_PERM_CONDITIONAL ? QF_FOUND_C
-                  : jr == kResErr ? QF_ERR : 0u;
-  if (fbit) atomicOr(&P->flags, fbit);
-  atomicSub(&P->pending, 1);
-  return true;
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
-  return v;
-}
-
-// Enumerate every lane's row (csr, begin, len) with all 64 lanes: edge t of the wave-wide
-// concatenation is read by lane t % 64 (consecutive edges of a row -> consecutive lanes).
-__device__ void b_distribute(const Ctx& c, const BCtx& b, int lane, uint32_t csr, uint32_t begin,
-                             uint32_t len, uint32_t q, uint16_t tgt, uint32_t depth, uint32_t cond,
-                             unsigned long long& edges, unsigned long long& ext_edges) {
-  WaveLDS* L = b.L;
-  const uint32_t incl = wave_incl_scan(len, lane);
-  const uint32_t total = __shfl(incl, 63, 64);
-  if (total == 0) return;
-  L->s_excl[lane] = incl - len;
-  L->s_begin[lane] = begin;
-  L->s_csr[lane] = csr;
-  L->s_q[lane] = q | (cond << 31);
-  L->s_tgt[lane] = tgt | (depth << 16);
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staging visible to the wave
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-    const uint32_t t = t0 + lane;
-    if (t < total) {
-      // source lane: last lane s with s_excl[s] <= t (lanes with len 0 share their successor's
-      // excl, so the last such lane is the one that owns edge t)
-      uint32_t lo = 0, hi = 63;
-      while (lo < hi) {
-        uint32_t mid = (lo + hi + 1) >> 1;
-        if (L->s_excl[mid] <= t) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t s = lo;
-      const uint32_t off = t - L->s_excl[s];
-      const DevCSR& r = c.csrs[L->s_csr[s]];
-      const uint32_t p = L->s_begin[s] + off;
-      const uint32_t x = r.nbr[p];
-      const uint32_t sq = L->s_q[s];
-      const uint32_t st = L->s_tgt[s];
-      uint32_t cnd = sq >> 31;
-      bool ok = true;
-      ++edges;
-      if (r.is_ext) {
-        ++ext_edges;
-        ok = visible(r, p, c.now_us);
-        cnd |= (r.cav[p] != 0);
-      }
-      if (ok && x != kWildcard && !(lds_ld(&L->q[sq & 0x7FFFFFFFu].flags) & QF_DONE))
-        b_push(b, sq & 0x7FFFFFFFu, x, (uint16_t)(st & 0xFFFF), st >> 16, cnd);
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-__global__ void __launch_bounds__(kBlock) k_bundles(Ctx c, BundleArgs a) {
-  __shared__ WaveLDS lds[kWaves];
-  const int w = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  WaveLDS* L = &lds[w];
-  const uint32_t slot = blockIdx.x * kWaves + w;
-  Entry* FA = a.fr_base + (size_t)slot * 2 * a.FC;
-  Entry* FB = FA + a.FC;
-  unsigned long long* V = a.vis_base + (size_t)slot * (a.vmask + 1);
-  unsigned long long s_rows = 0, s_probes = 0, s_edges = 0, s_ext = 0, s_exp = 0;
-
-  for (;;) {
-    uint32_t bi = 0;
-    if (lane == 0) bi = atomicAdd(a.bundle_ctr, 1u);
-    bi = __shfl(bi, 0, 64);
-    const uint32_t first = bi * a.B;
-    if (first >= a.n) break;
-    const uint32_t nb = min(a.B, a.n - first);
-    // epoch of this wave slot's visited table (a wrap clears the table)
-    uint32_t epoch = 0;
-    if (lane == 0) {
-      epoch = a.slot_epoch[slot] + 1;
-      if (epoch > kEpochMax) epoch = 0;
-      a.slot_epoch[slot] = epoch == 0 ? 1 : epoch;
-    }
-    epoch = __shfl(epoch, 0, 64);
-    if (epoch == 0) {
-      for (uint32_t h = lane; h <= a.vmask; h += 64) V[h] = 0ull;
-      __builtin_amdgcn_s_waitcnt(0);
-      epoch = 1;
-    }
-    BCtx b;
-    b.L = L;
-    b.V = V;
-    b.vmask = a.vmask;
-    b.FC = a.FC;
-    b.epoch = epoch;
-    b.level = 0;
-    // init the bundle's checks (lanes < nb)
-    if (lane == 0) {
-      L->q_count = nb;
-      L->j_count = 0;
-      L->overflow = 0;
-      L->next_n = 0;
-    }
-    if ((uint32_t)lane < nb) {
-      const gck_item it = a.items[first + lane];
-      int32_t err = GCK_ITEM_OK;
-      if (it.resource_type >= c.n_types || it.subject_type >= c.n_types) {
-        err = GCK_ITEM_ERR_UNKNOWN_TYPE;
-      } else if (it.permission >= c.n_rels || c.nodes[it.permission].type != it.resource_type) {
-        err = GCK_ITEM_ERR_UNKNOWN_PERMISSION;
-      } else if (it.subject_relation != kEllipsis &&
-                 (it.subject_relation >= c.n_rels || c.nodes[it.subject_relation].type != it.subject_type)) {
-        err = GCK_ITEM_ERR_UNKNOWN_SUBJECT_RELATION;
-      } else if (it.subject_id == kWildcard) {
-        err = GCK_ITEM_ERR_WILDCARD_SUBJECT;
-      }
-      L->err[lane] = err;
-      DevCheck ck;
-      ck.sid = it.subject_id;
-      ck.stype = it.subject_type;
-      ck.srel = it.subject_relation;
-      L->chk[lane] = ck;
-      LQuery q;
-      q.flags = 0;
-      q.pending = 0;
-      q.last_alive = 0;
-      q.parent_join = kNoJoin;
-      q.operand = 0;
-      q.check = lane;
-      if (err != GCK_ITEM_OK) {
-        q.flags = QF_DONE | (kResErr << QF_RES_SHIFT);
-      } else if (it.resource_id >= c.type_counts[it.resource_type]) {
-        bool ident = it.resource_type == it.subject_type && it.permission == it.subject_relation &&
-                     it.resource_id == it.subject_id && it.resource_id != kAbsent;
-        q.flags = QF_DONE | ((ident ? GCK_PERM_HAS : GCK_PERM_NO) << QF_RES_SHIFT);
-      }
-      L->q[lane] = q;
-      Entry e;
-      e.q = lane;
-      e.obj = it.resource_id;
-      e.node = it.permission;
-      e.depth = 0;
-      e.cond = 0;
-      FA[lane] = e;
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-
-    Entry* cur = FA;
-    Entry* nxt = FB;
-    uint32_t n = nb;
-    for (uint32_t level = 0; n > 0; ++level) {
-      b.level = level;
-      b.next = nxt;
-      if (lane == 0) L->next_n = 0;
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t i = base + lane;
-        bool act = i < n;
-        Entry e{};
-        DevNode nd{};
-        DevCheck s{};
-        if (act) {
-          e = cur[i];
-          act = !(lds_ld(&L->q[e.q].flags) & QF_DONE);
-        }
-        if (act) {
-          ++s_exp;
-          s = L->chk[L->q[e.q].check];
-          nd = c.nodes[e.node];
-          if ((nd.flags & NF_REAL) && e.node == s.srel && nd.type == s.stype && e.obj == s.sid) {
-            atomicOr(&L->q[e.q].flags, e.cond ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
-            act = false;
-          } else if (e.depth >= c.max_depth) {
-            atomicOr(&L->q[e.q].flags, (uint32_t)QF_ERR);
-            act = false;
-          }
-        }
-        uint32_t rows = 0, probes = 0;
-        if (act && nd.kind == NK_RELATION) {
-          // membership: the subject itself or a wildcard (checkDirect)
-          bool done = false;
-          for (uint32_t k = 0; k < nd.count && !done; ++k) {
-            const DevItem it = c.items[nd.first + k];
-            if (it.stype != s.stype) continue;
-            const bool direct = it.srel == s.srel;
-            const bool wild = it.srel == kEllipsis && s.srel == kEllipsis;
-            if (!direct && !wild) continue;
-            for (int pass = 0; pass < 2 && !done; ++pass) {
-              uint32_t ci = pass ? it.csr_ext : it.csr_plain;
-              if (ci == kNone) continue;
-              const DevCSR& r = c.csrs[ci];
-              if (e.obj >= r.n_rows) continue;
-              ++rows;
-              if (direct) {
-                uint32_t p = row_find(r, e.obj, s.sid, probes);
-                if (p != kNone && visible(r, p, c.now_us)) {
-                  uint32_t cnd = e.cond | (r.is_ext ? (r.cav[p] != 0) : 0u);
-                  atomicOr(&L->q[e.q].flags, cnd ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
-                  if (!cnd) done = true;
-                }
-              }
-              if (wild && !done) {
-                uint32_t bb = r.off[e.obj], en = r.off[e.obj + 1];
-                ++probes;
-                if (en > bb && r.nbr[en - 1] == kWildcard && visible(r, en - 1, c.now_us)) {
-                  uint32_t cnd = e.cond | (r.is_ext ? (r.cav[en - 1] != 0) : 0u);
-                  atomicOr(&L->q[e.q].flags, cnd ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
-                  if (!cnd) done = true;
-                }
-              }
-            }
-          }
-          if (done) act = false;
-        }
-        if (act && (nd.kind == NK_INTERSECT || nd.kind == NK_EXCLUDE || nd.kind == NK_ARROW_ALL)) {
-          b_spawn(c, b, e.q, e.obj, e.node, e.depth, e.cond, rows);
-          act = false;
-        }
-        // children: computed usersets pushed directly; userset / arrow rows distributed
-        const uint32_t kmax = wave_max(act ? nd.count : 0u);
-        for (uint32_t k = 0; k < kmax; ++k) {
-          uint32_t seg_csr[2] = {kNone, kNone};
-          uint16_t tgt = kNoNode;
-          if (act && k < nd.count) {
-            const DevItem it = c.items[nd.first + k];
-            if (nd.kind == NK_RELATION) {
-              if (it.srel != kEllipsis) {
-                seg_csr[0] = it.csr_plain;
-                seg_csr[1] = it.csr_ext;
-                tgt = it.target;
-              }
-            } else if (nd.kind == NK_UNION) {
-              if (it.kind == IT_COMPUTED) {
-                b_push(b, e.q, e.obj, it.target, e.depth + 1u, e.cond);
-              } else if (it.kind == IT_ARROW) {
-                seg_csr[0] = it.csr_plain;
-                seg_csr[1] = it.csr_ext;
-                tgt = it.target;
-              } else if (it.kind == IT_SUB) {
-                b_spawn(c, b, e.q, e.obj, it.target, e.depth, e.cond, rows);
-              }
-            }
-          }
-          for (int pass = 0; pass < 2; ++pass) {
-            uint32_t ci = seg_csr[pass];
-            uint32_t begin = 0, len = 0;
-            if (ci != kNone && tgt != kNoNode) {
-              const DevCSR& r = c.csrs[ci];
-              if (e.obj < r.n_rows) {
-                ++rows;
-                begin = r.off[e.obj];
-                len = r.off[e.obj + 1] - begin;
-              }
-            }
-            b_distribute(c, b, lane, ci == kNone ? 0u : ci, begin, len, e.q, tgt, e.depth + 1u, e.cond,
-                         s_edges, s_ext);
-          }
-        }
-        s_rows += rows;
-        s_probes += probes;
-      }
-      // resolve: decide queries, cascade through joins until stable. Not after an overflow:
-      // a dropped push would read as "no live entries" and decide a query too early.
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      if (L->overflow) break;
-      for (int iter = 0; iter < kBQ + 2; ++iter) {
-        const uint32_t qn = min(L->q_count, (uint32_t)kBQ);
-        bool changed = false;
-        for (uint32_t qb = 0; qb < qn; qb += 64) {
-          const uint32_t qi = qb + lane;
-          if (qi < qn) {
-            const uint32_t f = lds_ld(&L->q[qi].flags);
-            if (!(f & QF_DONE)) {
-              if (f & QF_FOUND_Y) {
-                changed |= b_finalize(L, qi, GCK_PERM_HAS);
-              } else if (lds_ld(&L->q[qi].last_alive) <= level && lds_ld(&L->q[qi].pending) == 0) {
-                // re-read: a sibling lane may have resolved this query's last join (its
-                // contribution is written before the pending decrement we just observed)
-                changed |= b_finalize(L, qi, result_from_flags(lds_ld(&L->q[qi].flags)));
-              }
-            }
-          }
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-          __builtin_amdgcn_wave_barrier();
-        }
-        if (!__any(changed)) break;
-      }
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      uint32_t nn = L->next_n;
-      if (L->overflow) break;
-      n = nn;
-      Entry* t = cur;
-      cur = nxt;
-      nxt = t;
-    }
-    if (a.dbg && bi == 0) {  // debug dump of bundle 0's final query/join tables
-      const uint32_t qn = min(L->q_count, (uint32_t)kBQ), jn = min(L->j_count, (uint32_t)kBJ);
-      for (uint32_t k = lane; k < qn; k += 64) {
-        uint32_t* d = a.dbg + 4 + k * 6;
-        d[0] = L->q[k].flags; d[1] = (uint32_t)L->q[k].pending; d[2] = L->q[k].last_alive;
-        d[3] = L->q[k].parent_join; d[4] = L->q[k].operand; d[5] = L->q[k].check;
-      }
-      for (uint32_t k = lane; k < jn; k += 64) {
-        uint32_t* d = a.dbg + 4 + kBQ * 6 + k * 8;
-        d[0] = L->j[k].parent_q; d[1] = L->j[k].first_child; d[2] = L->j[k].n_ops; d[3] = L->j[k].op;
-        d[4] = L->j[k].cond; d[5] = L->j[k].state; d[6] = (uint32_t)L->j[k].remaining;
-      }
-      if (lane == 0) { a.dbg[0] = qn; a.dbg[1] = jn; a.dbg[2] = L->overflow; a.dbg[3] = epoch; }
-    }
-    // outputs (undecided checks after an overflow are deferred to the grid-wide path)
-    const bool ovf = L->overflow != 0;
-    if ((uint32_t)lane < nb) {
-      const uint32_t f = L->q[lane].flags;
-      const uint32_t idx = first + lane;
-      if (f & QF_DONE) {
-        uint32_t res = (f >> QF_RES_SHIFT) & 0xF;
-        int32_t err = L->err[lane];
-        if (err == GCK_ITEM_OK && res == kResErr) err = GCK_ITEM_ERR_MAX_DEPTH;
-        a.out_perm[idx] = (err != GCK_ITEM_OK) ? (uint8_t)GCK_PERM_UNSPECIFIED : (uint8_t)res;
-        a.out_err[idx] = err;
-      } else {
-        a.deferred[atomicAdd(a.n_deferred, 1u)] = idx;
-        if (!ovf) a.out_err[idx] = -1;  // invariant violated; reported by the host
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-  }
-  wave_add(&c.ctr->row_lookups, s_rows);
-  wave_add(&c.ctr->probes, s_probes);
-  wave_add(&c.ctr->edges, s_edges);
-  wave_add(&c.ctr->ext_edges, s_ext);
-  wave_add(&c.ctr->expanded, s_exp);
 }
 
 __global__ void __launch_bounds__(kBlock) k_gather(const gck_item* __restrict__ items,
@@ -1389,8 +834,22 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
         d.cav = cav;
         d.exp_us = ex;
       }
+      // hashed membership index for plain direct-subject kinds (the check
+      // "is this subject in the row" becomes one probe instead of a binary search)
+      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+        const uint64_t slots = 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne));
+        unsigned long long* tab = dalloc<unsigned long long>(ds->allocs, slots, &ds->bytes);
+        HIP_OK(hipMemset(tab, 0xFF, slots * sizeof(unsigned long long)));
+        const uint64_t blocks = (ne + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(k_build_mhash, dim3((uint32_t)blocks), dim3(kBlock), 0, 0, off, nbr, h.n_rows,
+                           (unsigned long long)ne, tab, (unsigned long long)(slots - 1));
+        HIP_OK(hipGetLastError());
+        d.mhash = tab;
+        d.mmask = slots - 1;
+      }
       table.push_back(d);
     }
+    HIP_OK(hipDeviceSynchronize());
     // link the node program to the CSR table
     std::vector<DevItem> items = sc.items;
     for (size_t i = 0; i < items.size(); ++i) {
@@ -1475,15 +934,23 @@ static Workspace* ensure_workspace(Engine& e) {
       const uint32_t wpc = cf.bundle_waves_per_cu ? cf.bundle_waves_per_cu : 16;
       w->b_checks = cf.bundle_checks ? std::min<uint32_t>(cf.bundle_checks, kBMax) : 16;
       w->b_fc = cf.bundle_frontier ? cf.bundle_frontier : 4096;
-      w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 8192);
+      w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 16384);
       w->b_blocks = std::max<uint32_t>(1, (uint32_t)cus * wpc / kWaves);
       const size_t slots = (size_t)w->b_blocks * kWaves;
       w->b_fr = dalloc<Entry>(w->allocs, slots * 2 * w->b_fc);
       w->b_vis = dalloc<unsigned long long>(w->allocs, slots * w->b_vslots);
-      w->b_epoch = dalloc<uint32_t>(w->allocs, slots);
+      w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots);
       HIP_OK(hipMemset(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long)));
-      HIP_OK(hipMemset(w->b_epoch, 0, slots * sizeof(uint32_t)));
       w->b_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
+      w->b_budget = cf.bundle_budget ? cf.bundle_budget : 1024;
+      w->g_fc = cf.giant_frontier ? cf.giant_frontier : 65536;
+      w->g_vslots = 1u << ceil_log2(cf.giant_visited ? cf.giant_visited : 262144);
+      w->g_slots = cf.giant_slots ? cf.giant_slots : (uint32_t)cus;
+      w->g_fr = dalloc<Entry>(w->allocs, (size_t)w->g_slots * 2 * w->g_fc);
+      w->g_vis = dalloc<unsigned long long>(w->allocs, (size_t)w->g_slots * w->g_vslots);
+      w->g_vlog = dalloc<uint32_t>(w->allocs, (size_t)w->g_slots * w->g_vslots);
+      HIP_OK(hipMemset(w->g_vis, 0, (size_t)w->g_slots * w->g_vslots * sizeof(unsigned long long)));
+      w->g_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
       w->b_ctrs = dalloc<unsigned>(w->allocs, 4);
       w->def_items = dalloc<gck_item>(w->allocs, w->max_batch);
       w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
@@ -1645,19 +1112,55 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   a.vmask = w.b_vslots - 1;
   a.fr_base = w.b_fr;
   a.vis_base = w.b_vis;
-  a.slot_epoch = w.b_epoch;
+  a.vlog_base = w.b_vlog;
   static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
   static uint32_t* dbg = nullptr;
   const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;
   if (dbg_on && !dbg) HIP_OK(hipMalloc(&dbg, dbg_words * 4));
   a.dbg = dbg_on ? dbg : nullptr;
+  a.budget = w.b_budget;
+  a.idx = nullptr;
+  a.n_dev = nullptr;
+  // GCK_DEBUG_TIMING=<file prefix>: per-bundle {start, end, levels, entries} of both stages
+  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  static unsigned long long* timing = nullptr;
+  const size_t timing_words = 4ull * (n + 1) * 2;
+  static size_t timing_cap = 0;
+  if (timing_env && timing_cap < timing_words) {
+    if (timing) (void)hipFree(timing);
+    HIP_OK(hipMalloc(&timing, timing_words * 8));
+    timing_cap = timing_words;
+  }
+  a.timing = timing_env ? timing : nullptr;
+  // stage B: giant checks, one 16-wave workgroup each, over stage A's deferred list (its length
+  // is read on the device, so both stages are queued back to back without a host round trip)
+  BundleArgs g = a;
+  g.idx = w.b_deferred;
+  g.n = n;
+  g.n_dev = w.b_ctrs + 1;
+  g.deferred = w.g_deferred;
+  g.n_deferred = w.b_ctrs + 3;
+  g.bundle_ctr = w.b_ctrs + 2;
+  g.B = 1;
+  g.FC = w.g_fc;
+  g.vmask = w.g_vslots - 1;
+  g.budget = 0xFFFFFFFFu;
+  g.fr_base = w.g_fr;
+  g.vis_base = w.g_vis;
+  g.vlog_base = w.g_vlog;
+  g.dbg = nullptr;
+  g.timing = timing_env ? timing + 4ull * (n + 1) : nullptr;
+  if (timing_env) HIP_OK(hipMemsetAsync(timing, 0, timing_words * 8, st));
   HIP_OK(hipEventRecord(w.ev0, st));
   HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
   HIP_OK(hipMemsetAsync(w.b_ctrs, 0, 4 * sizeof(unsigned), st));
   if (profile) HIP_OK(hipEventRecord(w.pev[0], st));
-  hipLaunchKernelGGL(k_bundles, dim3(w.b_blocks), dim3(kBlock), 0, st, c, a);
+  hipLaunchKernelGGL(k_bundles<1>, dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
   HIP_OK(hipGetLastError());
   if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
+  hipLaunchKernelGGL(k_bundles<kGiantWaves>, dim3(w.g_slots), dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
+  HIP_OK(hipGetLastError());
+  if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
   HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(w.h_bctrs, w.b_ctrs, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIP_OK(hipEventRecord(w.ev1, st));
@@ -1666,9 +1169,11 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   HIP_OK(hipEventElapsedTime(&ms, w.ev0, w.ev1));
   *ms_out += ms;
   if (profile) {
-    float b = 0.f;
+    float b = 0.f, gm = 0.f;
     HIP_OK(hipEventElapsedTime(&b, w.pev[0], w.pev[1]));
+    HIP_OK(hipEventElapsedTime(&gm, w.pev[1], w.pev[2]));
     e.stats.bundle_ms += b;
+    e.stats.giant_ms += gm;
     e.stats.bundle_launches++;
   }
   const DevCounters& h = *w.h_ctr;
@@ -1694,15 +1199,28 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
               d[2], d[3], d[4], d[5], (int)d[6]);
     }
   }
-  const uint32_t n_def = w.h_bctrs[1];
-  if (n_def > n) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
-  if (n_def == 0) return;
+  if (timing_env) {  // append both stages' per-bundle records to <prefix>.bin (u64 x4 each)
+    std::vector<unsigned long long> h(timing_words);
+    HIP_OK(hipMemcpy(h.data(), timing, timing_words * 8, hipMemcpyDeviceToHost));
+    std::string path = std::string(timing_env) + ".bin";
+    if (FILE* f = fopen(path.c_str(), "ab")) {
+      unsigned long long hdr[4] = {0xB0DDull, n, w.b_checks, w.h_bctrs[1]};
+      fwrite(hdr, 8, 4, f);
+      fwrite(h.data(), 8, timing_words, f);
+      fclose(f);
+    }
+  }
+  const uint32_t n_def = w.h_bctrs[1], n_def2 = w.h_bctrs[3];
+  if (n_def > n || n_def2 > n_def) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
   e.stats.deferred += n_def;
-  const uint32_t grid = (n_def + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, w.b_deferred, n_def, w.def_items);
+  e.stats.deferred_wide += n_def2;
+  if (n_def2 == 0) return;
+  // stage C: the grid-wide level-synchronous path for what outgrew a workgroup bundle
+  const uint32_t grid = (n_def2 + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, w.g_deferred, n_def2, w.def_items);
   HIP_OK(hipGetLastError());
-  check_range_wide(e, w, w.def_items, n_def, now_us, w.def_perm, w.def_err, st, ms_out);
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, w.b_deferred, n_def, w.def_perm, w.def_err,
+  check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, ms_out);
+  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, w.g_deferred, n_def2, w.def_perm, w.def_err,
                      d_perm, d_err);
   HIP_OK(hipGetLastError());
   HIP_OK(hipStreamSynchronize(st));

@@ -66,6 +66,10 @@ struct DevCSR {
   const int64_t* exp_us;  // ext only
   uint32_t n_rows;
   uint32_t is_ext;
+  // membership index of a plain direct-subject CSR: open-addressing set of
+  // (object << 32 | subject) keys, 2x oversized, linear probing (nullptr = none)
+  const unsigned long long* mhash;
+  unsigned long long mmask;
 };
 
 // ---- per-batch state ----------------------------------------------------------------------

@@ -81,6 +81,7 @@ extern "C" {
 #define GCK_MEM_DEVICE 1u        /* gck_load_csr: pointers are device memory */
 #define GCK_FLAG_PROFILE 1u      /* gck_config.flags: time every kernel with HIP events */
 #define GCK_FLAG_NO_BUNDLE 2u    /* gck_config.flags: grid-wide level-synchronous path only */
+#define GCK_FLAG_NO_MHASH 4u     /* gck_config.flags: no hashed membership index (binary search) */
 
 typedef struct gck_engine gck_engine;
 
@@ -97,6 +98,11 @@ typedef struct gck_config {
   uint32_t bundle_frontier;    /* frontier entries per wavefront; 0 = 4096 */
   uint32_t bundle_visited;     /* visited slots per wavefront (power of 2); 0 = 8192 */
   uint32_t bundle_waves_per_cu;/* resident wavefronts per CU for the bundle kernel; 0 = 16 */
+  uint32_t bundle_budget;      /* entries one check may push in a wavefront bundle before it is
+                                  handed to a 16-wave workgroup; 0 = 1024 */
+  uint32_t giant_frontier;     /* frontier entries per 16-wave workgroup bundle; 0 = 65536 */
+  uint32_t giant_visited;      /* visited slots per workgroup bundle (power of 2); 0 = 262144 */
+  uint32_t giant_slots;        /* resident workgroup bundles; 0 = one per CU */
 } gck_config;
 
 /* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
@@ -145,9 +151,11 @@ typedef struct gck_stats {
   double resolve_ms;           /* GCK_FLAG_PROFILE: summed k_resolve time */
   uint64_t expand_launches;    /* GCK_FLAG_PROFILE: k_expand launches timed */
   uint64_t edges_launches;     /* GCK_FLAG_PROFILE: k_edges launches timed */
-  double bundle_ms;            /* GCK_FLAG_PROFILE: summed k_bundles time */
-  uint64_t bundle_launches;    /* GCK_FLAG_PROFILE: k_bundles launches timed */
-  uint64_t deferred;           /* checks re-run by the grid-wide path after a bundle overflow */
+  double bundle_ms;            /* GCK_FLAG_PROFILE: summed wavefront-bundle kernel time */
+  uint64_t bundle_launches;    /* GCK_FLAG_PROFILE: bundle launches timed */
+  uint64_t deferred;           /* checks handed from wavefront bundles to workgroup bundles */
+  double giant_ms;             /* GCK_FLAG_PROFILE: summed workgroup-bundle kernel time */
+  uint64_t deferred_wide;      /* checks handed from workgroup bundles to the grid-wide path */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

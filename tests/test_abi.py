@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert E.ITEM_DTYPE.itemsize == 20
     assert E.TUPLE_DTYPE.itemsize == 32
-    assert C.sizeof(E._Config) == 64
+    assert C.sizeof(E._Config) == 80
     assert E.load_library().gck_abi_version() == 1
 
 

@@ -152,10 +152,17 @@ PATHS = {
     "bundle": {},
     # grid-wide level-synchronous kernels only
     "wide": {"wide_only": True},
-    # tiny per-wave scratch: most bundles overflow and are re-run by the grid-wide path
+    # tiny per-wave scratch: most bundles overflow and are re-run by the later stages
     "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 16},
+    # tiny work budget: almost every check is handed to a 16-wave workgroup bundle
+    "giant": {"bundle_budget": 2},
+    # ... and those overflow their workgroup scratch into the grid-wide path
+    "giant-deferred": {"bundle_budget": 2, "giant_frontier": 8, "giant_visited": 16, "giant_slots": 3},
     # one check per wavefront, few resident waves
     "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4},
+    # binary-search membership instead of the hashed index, both paths
+    "nohash": {"membership_hash": False},
+    "nohash-wide": {"membership_hash": False, "wide_only": True},
 }
 
 
