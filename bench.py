@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--bundle-budget", type=int, default=0)
     ap.add_argument("--giant-slots", type=int, default=0)
     ap.add_argument("--wide-only", action="store_true")
+    ap.add_argument("--no-giant", action="store_true", help="deferred checks go to the grid-wide path")
     return ap.parse_args()
 
 
@@ -74,7 +75,8 @@ def main():
     eng = Engine(device=local, profile=not args.no_profile, wide_only=args.wide_only,
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
-                 bundle_budget=args.bundle_budget, giant_slots=args.giant_slots)
+                 bundle_budget=args.bundle_budget, giant_slots=args.giant_slots,
+                 giant_stage=not args.no_giant)
     eng.load_schema(synth.SCHEMA)
     assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
     assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "engine.hpp"
 
@@ -74,7 +75,7 @@ struct Workspace {
   hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // GCK_FLAG_PROFILE
   // bundle path
   uint32_t b_checks = 16, b_fc = 4096, b_vslots = 16384, b_blocks = 0;
-  Entry* b_fr = nullptr;
+  unsigned long long* b_fr = nullptr;  // packed frontier entries beyond the LDS part
   unsigned long long* b_vis = nullptr;
   uint32_t* b_vlog = nullptr;  // per slot: claimed visited slots (cleared by the bundle)
   uint32_t* b_deferred = nullptr;
@@ -83,7 +84,7 @@ struct Workspace {
   uint32_t b_budget = 1024;
   // giant-check stage: one 16-wave workgroup per bundle
   uint32_t g_fc = 65536, g_vslots = 262144, g_slots = 0;
-  Entry* g_fr = nullptr;
+  unsigned long long* g_fr = nullptr;
   unsigned long long* g_vis = nullptr;
   uint32_t* g_vlog = nullptr;
   uint32_t* g_deferred = nullptr;
@@ -101,6 +102,7 @@ struct Ctx {
   const DevCSR* csrs;
   const uint32_t* type_counts;
   uint32_t n_types, n_rels;
+  uint32_t n_nodes, n_items, n_csrs;
   DevCheck* checks;
   DevQuery* queries;
   DevJoin* joins;
@@ -210,17 +212,46 @@ __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t n
   return x == 0 || x > now_us;
 }
 
-// Is (obj, sid) in the membership index? One dependent line in the common case.
-__device__ __forceinline__ bool hash_member(const DevCSR& r, uint32_t obj, uint32_t sid, uint32_t& probes) {
-  const unsigned long long key = ((unsigned long long)obj << 32) | sid;
-  unsigned long long h = mix64(key) & r.mmask;
-  for (;;) {
+// Membership-index bucket scan: 1 = key present, 0 = absent (the bucket has an empty slot, so
+// no key homed here overflowed), 2 = bucket full without the key (continue with the next one).
+constexpr int kBucketKeys = 8;  // 8 x u64 = 64 B
+
+__device__ __forceinline__ uint32_t bucket_probe(const unsigned long long* tab, uint32_t b,
+                                                 unsigned long long key) {
+  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(tab + (size_t)b * kBucketKeys);
+  const ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+  const bool hit = a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key ||
+                   a2.y == key || a3.x == key || a3.y == key;
+  const bool empty = a0.x == kEmptyKey || a0.y == kEmptyKey || a1.x == kEmptyKey || a1.y == kEmptyKey ||
+                     a2.x == kEmptyKey || a2.y == kEmptyKey || a3.x == kEmptyKey || a3.y == kEmptyKey;
+  return hit ? 1u : empty ? 0u : 2u;
+}
+
+__device__ __forceinline__ unsigned long long mkey(uint32_t obj, uint32_t sid) {
+  return ((unsigned long long)obj << 32) | sid;
+}
+
+__device__ __forceinline__ uint32_t mbucket(const DevCSR& r, unsigned long long key) {
+  return (uint32_t)(mix64(key) & r.mmask);
+}
+
+// Continue a lookup whose bucket b answered `v` (0/1/2, bucket_probe).
+__device__ __forceinline__ bool mhash_finish(const DevCSR& r, uint32_t b, unsigned long long key, uint32_t v,
+                                             uint32_t& probes) {
+  while (v == 2u) {
+    b = (uint32_t)((b + 1) & r.mmask);
+    v = bucket_probe(r.mhash, b, key);
     ++probes;
-    const unsigned long long v = r.mhash[h];
-    if (v == key) return true;
-    if (v == kEmptyKey) return false;
-    h = (h + 1) & r.mmask;
   }
+  return v == 1u;
+}
+
+// Is (obj, sid) in the membership index? One 64-byte bucket read in the common case.
+__device__ __forceinline__ bool hash_member(const DevCSR& r, uint32_t obj, uint32_t sid, uint32_t& probes) {
+  const unsigned long long key = mkey(obj, sid);
+  const uint32_t b = mbucket(r, key);
+  ++probes;
+  return mhash_finish(r, b, key, bucket_probe(r.mhash, b, key), probes);
 }
 
 // checkDirect membership on one CSR: the subject itself (`direct`) and/or the wildcard
@@ -231,7 +262,7 @@ __device__ __forceinline__ uint32_t member_test(const DevCSR& r, uint32_t obj, u
   if (obj >= r.n_rows) return 0;
   if (r.mhash) {  // plain direct CSR: hashed index, no row read
     if (direct && hash_member(r, obj, sid, probes)) return 1;
-    if (wild && hash_member(r, obj, kWildcard, probes)) return 1;
+    if (wild && r.has_wild && hash_member(r, obj, kWildcard, probes)) return 1;
     return 0;
   }
   ++rows;
@@ -686,12 +717,14 @@ constexpr int kWaves = kBlock / 64;
 
 // Membership index build: one lane per edge of a plain direct-subject CSR. Each block owns 256
 // consecutive edges; two lanes find the block's first and last rows, then every lane finds its
-// row in that (usually 1-2 row) window.
+// row in that (usually 1-2 row) window. A key takes the first empty slot of its home bucket or,
+// when that is full, of the next buckets in turn (the lookup rule in bucket_probe). Also flags
+// whether any row holds the wildcard subject.
 __global__ void __launch_bounds__(kBlock) k_build_mhash(const uint32_t* __restrict__ off,
                                                         const uint32_t* __restrict__ nbr, uint32_t n_rows,
                                                         unsigned long long n_edges,
                                                         unsigned long long* __restrict__ tab,
-                                                        unsigned long long mask) {
+                                                        unsigned long long bmask, unsigned* has_wild) {
   __shared__ uint32_t rows[2];
   const unsigned long long e0 = (unsigned long long)blockIdx.x * kBlock;
   if (threadIdx.x < 2) {
@@ -713,12 +746,21 @@ __global__ void __launch_bounds__(kBlock) k_build_mhash(const uint32_t* __restri
     if (off[mid] <= e) lo = mid;
     else hi = mid - 1;
   }
-  const unsigned long long key = ((unsigned long long)lo << 32) | nbr[e];
-  unsigned long long h = mix64(key) & mask;
+  const uint32_t sid = nbr[e];
+  if (sid == kWildcard) atomicOr(has_wild, 1u);
+  const unsigned long long key = mkey(lo, sid);
+  unsigned long long b = mix64(key) & bmask;
   for (;;) {
-    const unsigned long long prev = atomicCAS(&tab[h], kEmptyKey, key);
-    if (prev == kEmptyKey || prev == key) return;
-    h = (h + 1) & mask;
+    unsigned long long* bk = tab + b * kBucketKeys;
+    for (int k = 0; k < kBucketKeys; ++k) {
+      unsigned long long v = __hip_atomic_load(&bk[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == key) return;
+      if (v == kEmptyKey) {
+        v = atomicCAS(&bk[k], kEmptyKey, key);
+        if (v == kEmptyKey || v == key) return;
+      }
+    }
+    b = (b + 1) & bmask;
   }
 }
 
@@ -808,10 +850,11 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
   auto* ds = new DeviceSnapshot();
   try {
     std::vector<DevCSR> table;
+    unsigned* wild_flag = dalloc<unsigned>(ds->allocs, 1);
     for (HostCSR& h : csrs) {
       DevCSR d{};
       d.n_rows = h.n_rows;
-      d.is_ext = h.ext ? 1u : 0u;
+      d.is_ext = h.ext ? 1 : 0;
       uint64_t ne = h.dev_off ? h.n_edges : h.nbr.size();
       uint32_t* off = dalloc<uint32_t>(ds->allocs, (size_t)h.n_rows + 1, &ds->bytes);
       uint32_t* nbr = dalloc<uint32_t>(ds->allocs, ne, &ds->bytes);
@@ -838,14 +881,19 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       // "is this subject in the row" becomes one probe instead of a binary search)
       if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
         const uint64_t slots = 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne));
+        if (slots / kBucketKeys > (1ull << 32)) throw Error(GCK_E_CAPACITY, "membership index too large");
         unsigned long long* tab = dalloc<unsigned long long>(ds->allocs, slots, &ds->bytes);
         HIP_OK(hipMemset(tab, 0xFF, slots * sizeof(unsigned long long)));
+        HIP_OK(hipMemset(wild_flag, 0, sizeof(unsigned)));
         const uint64_t blocks = (ne + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(k_build_mhash, dim3((uint32_t)blocks), dim3(kBlock), 0, 0, off, nbr, h.n_rows,
-                           (unsigned long long)ne, tab, (unsigned long long)(slots - 1));
+                           (unsigned long long)ne, tab, (unsigned long long)(slots / kBucketKeys - 1), wild_flag);
         HIP_OK(hipGetLastError());
+        unsigned hw = 0;
+        HIP_OK(hipMemcpy(&hw, wild_flag, sizeof(unsigned), hipMemcpyDeviceToHost));
         d.mhash = tab;
-        d.mmask = slots - 1;
+        d.mmask = slots / kBucketKeys - 1;
+        d.has_wild = hw ? 1 : 0;
       }
       table.push_back(d);
     }
@@ -937,7 +985,7 @@ static Workspace* ensure_workspace(Engine& e) {
       w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 16384);
       w->b_blocks = std::max<uint32_t>(1, (uint32_t)cus * wpc / kWaves);
       const size_t slots = (size_t)w->b_blocks * kWaves;
-      w->b_fr = dalloc<Entry>(w->allocs, slots * 2 * w->b_fc);
+      w->b_fr = dalloc<unsigned long long>(w->allocs, slots * 2 * w->b_fc);
       w->b_vis = dalloc<unsigned long long>(w->allocs, slots * w->b_vslots);
       w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots);
       HIP_OK(hipMemset(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long)));
@@ -946,7 +994,7 @@ static Workspace* ensure_workspace(Engine& e) {
       w->g_fc = cf.giant_frontier ? cf.giant_frontier : 65536;
       w->g_vslots = 1u << ceil_log2(cf.giant_visited ? cf.giant_visited : 262144);
       w->g_slots = cf.giant_slots ? cf.giant_slots : (uint32_t)cus;
-      w->g_fr = dalloc<Entry>(w->allocs, (size_t)w->g_slots * 2 * w->g_fc);
+      w->g_fr = dalloc<unsigned long long>(w->allocs, (size_t)w->g_slots * 2 * w->g_fc);
       w->g_vis = dalloc<unsigned long long>(w->allocs, (size_t)w->g_slots * w->g_vslots);
       w->g_vlog = dalloc<uint32_t>(w->allocs, (size_t)w->g_slots * w->g_vslots);
       HIP_OK(hipMemset(w->g_vis, 0, (size_t)w->g_slots * w->g_vslots * sizeof(unsigned long long)));
@@ -984,6 +1032,9 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.type_counts = ds.type_counts;
   c.n_types = ds.n_types;
   c.n_rels = ds.n_rels;
+  c.n_nodes = ds.n_nodes;
+  c.n_items = ds.n_items;
+  c.n_csrs = ds.n_csrs;
   c.checks = w.checks;
   c.queries = w.queries;
   c.joins = w.joins;
@@ -1121,10 +1172,10 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   a.budget = w.b_budget;
   a.idx = nullptr;
   a.n_dev = nullptr;
-  // GCK_DEBUG_TIMING=<file prefix>: per-bundle {start, end, levels, entries} of both stages
+  // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
   static unsigned long long* timing = nullptr;
-  const size_t timing_words = 4ull * (n + 1) * 2;
+  const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
   static size_t timing_cap = 0;
   if (timing_env && timing_cap < timing_words) {
     if (timing) (void)hipFree(timing);
@@ -1149,17 +1200,32 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   g.vis_base = w.g_vis;
   g.vlog_base = w.g_vlog;
   g.dbg = nullptr;
-  g.timing = timing_env ? timing + 4ull * (n + 1) : nullptr;
+  g.timing = timing_env ? timing + (size_t)kTimingWords * (n + 1) : nullptr;
   if (timing_env) HIP_OK(hipMemsetAsync(timing, 0, timing_words * 8, st));
   HIP_OK(hipEventRecord(w.ev0, st));
   HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
   HIP_OK(hipMemsetAsync(w.b_ctrs, 0, 4 * sizeof(unsigned), st));
   if (profile) HIP_OK(hipEventRecord(w.pev[0], st));
-  hipLaunchKernelGGL(k_bundles<1>, dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  // the node program is staged in LDS when it fits (bundle.inc)
+  const size_t prog_bytes = (size_t)c.n_csrs * sizeof(DevCSR) + (size_t)c.n_nodes * sizeof(DevNode) +
+                            (size_t)c.n_items * sizeof(DevItem);
+  const bool prog_lds = prog_bytes <= (size_t)kProgBytes;
+  if (prog_lds)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
   HIP_OK(hipGetLastError());
   if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
-  hipLaunchKernelGGL(k_bundles<kGiantWaves>, dim3(w.g_slots), dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
-  HIP_OK(hipGetLastError());
+  const bool giant = !(e.cfg.flags & GCK_FLAG_NO_GIANT);
+  if (giant) {
+    if (prog_lds)
+      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, true>), dim3(w.g_slots),
+                         dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
+    else
+      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, false>), dim3(w.g_slots),
+                         dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
+    HIP_OK(hipGetLastError());
+  }
   if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
   HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(w.h_bctrs, w.b_ctrs, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
@@ -1199,7 +1265,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
               d[2], d[3], d[4], d[5], (int)d[6]);
     }
   }
-  if (timing_env) {  // append both stages' per-bundle records to <prefix>.bin (u64 x4 each)
+  if (timing_env) {  // append both stages' per-bundle records to <prefix>.bin (kTimingWords u64 each)
     std::vector<unsigned long long> h(timing_words);
     HIP_OK(hipMemcpy(h.data(), timing, timing_words * 8, hipMemcpyDeviceToHost));
     std::string path = std::string(timing_env) + ".bin";
@@ -1210,17 +1276,18 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
       fclose(f);
     }
   }
-  const uint32_t n_def = w.h_bctrs[1], n_def2 = w.h_bctrs[3];
+  const uint32_t n_def = w.h_bctrs[1], n_def2 = giant ? w.h_bctrs[3] : n_def;
+  const uint32_t* def_idx = giant ? w.g_deferred : w.b_deferred;
   if (n_def > n || n_def2 > n_def) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
   e.stats.deferred += n_def;
   e.stats.deferred_wide += n_def2;
   if (n_def2 == 0) return;
   // stage C: the grid-wide level-synchronous path for what outgrew a workgroup bundle
   const uint32_t grid = (n_def2 + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, w.g_deferred, n_def2, w.def_items);
+  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, def_idx, n_def2, w.def_items);
   HIP_OK(hipGetLastError());
   check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, ms_out);
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, w.g_deferred, n_def2, w.def_perm, w.def_err,
+  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, def_idx, n_def2, w.def_perm, w.def_err,
                      d_perm, d_err);
   HIP_OK(hipGetLastError());
   HIP_OK(hipStreamSynchronize(st));

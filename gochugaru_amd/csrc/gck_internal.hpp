@@ -65,11 +65,14 @@ struct DevCSR {
   const uint32_t* cav;    // ext only
   const int64_t* exp_us;  // ext only
   uint32_t n_rows;
-  uint32_t is_ext;
+  uint8_t is_ext;
+  uint8_t has_wild;  // some row holds the wildcard subject (plain direct CSRs with an index)
+  uint16_t pad;
   // membership index of a plain direct-subject CSR: open-addressing set of
-  // (object << 32 | subject) keys, 2x oversized, linear probing (nullptr = none)
+  // (object << 32 | subject) keys, 2x oversized, in 64-byte buckets of 8 keys probed
+  // bucket-linearly (a lookup reads one bucket in the common case; nullptr = none)
   const unsigned long long* mhash;
-  unsigned long long mmask;
+  unsigned long long mmask;  // bucket count - 1
 };
 
 // ---- per-batch state ----------------------------------------------------------------------

@@ -47,6 +47,7 @@ MEM_DEVICE = 1
 FLAG_PROFILE = 1
 FLAG_NO_BUNDLE = 2
 FLAG_NO_MHASH = 4
+FLAG_NO_GIANT = 8
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -189,10 +190,10 @@ class Engine:
                  wide_only: bool = False, bundle_checks: int = 0, bundle_frontier: int = 0,
                  bundle_visited: int = 0, bundle_waves_per_cu: int = 0,
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
-                 giant_visited: int = 0, giant_slots: int = 0):
+                 giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
-                 | (0 if membership_hash else FLAG_NO_MHASH))
+                 | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,

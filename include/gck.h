@@ -82,6 +82,7 @@ extern "C" {
 #define GCK_FLAG_PROFILE 1u      /* gck_config.flags: time every kernel with HIP events */
 #define GCK_FLAG_NO_BUNDLE 2u    /* gck_config.flags: grid-wide level-synchronous path only */
 #define GCK_FLAG_NO_MHASH 4u     /* gck_config.flags: no hashed membership index (binary search) */
+#define GCK_FLAG_NO_GIANT 8u     /* gck_config.flags: deferred checks skip the workgroup-bundle stage */
 
 typedef struct gck_engine gck_engine;
 

@@ -4,6 +4,8 @@ import sys
 
 import numpy as np
 
+W = 12  # kTimingWords (bundle.inc)
+PHASES = ("load", "issue", "claim", "member", "children", "resolve")
 TICK_US = 0.01  # wall_clock64 runs at 100 MHz on MI300-class parts
 
 
@@ -13,8 +15,8 @@ def main(path):
     while pos < len(raw):
         assert raw[pos] == 0xB0DD, "bad header"
         n, B, ndef = int(raw[pos + 1]), int(raw[pos + 2]), int(raw[pos + 3])
-        words = 4 * (n + 1) * 2
-        rec = raw[pos + 4: pos + 4 + words].reshape(2, n + 1, 4)
+        words = W * (n + 1) * 2
+        rec = raw[pos + 4: pos + 4 + words].reshape(2, n + 1, W)
         batches.append((n, B, ndef, rec))
         pos += 4 + words
     n, B, ndef, rec = batches[-1]
@@ -36,6 +38,10 @@ def main(path):
                   f"entries={np.percentile(ent, q):7.1f} start={np.percentile(start, q):7.1f}us")
         per_level = dur / np.maximum(lv, 1)
         print(f"   us/level p50={np.percentile(per_level, 50):.2f} p90={np.percentile(per_level, 90):.2f}")
+        tot = r[:, 4:4 + len(PHASES)].sum(axis=0) * TICK_US
+        lvl = lv.sum()
+        print("   phase us/level (lane 0): " + " ".join(
+            f"{nm}={t / lvl:.2f}" for nm, t in zip(PHASES, tot)))
         # what ends last
         k = np.argsort(r[:, 1])[-5:]
         for i in k:

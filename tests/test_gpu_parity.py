@@ -158,6 +158,8 @@ PATHS = {
     "giant": {"bundle_budget": 2},
     # ... and those overflow their workgroup scratch into the grid-wide path
     "giant-deferred": {"bundle_budget": 2, "giant_frontier": 8, "giant_visited": 16, "giant_slots": 3},
+    # deferred checks straight to the grid-wide path
+    "giant-skip": {"bundle_budget": 2, "giant_stage": False},
     # one check per wavefront, few resident waves
     "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4},
     # binary-search membership instead of the hashed index, both paths

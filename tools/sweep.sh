@@ -1,0 +1,9 @@
+set -e
+mkdir -p gpurun_out/sw
+rm -f gpurun_out/sw/t.bin
+GCK_DEBUG_TIMING=gpurun_out/sw/t timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/sw/t.json 2> gpurun_out/sw/t.err
+python tests/analyze_timing.py gpurun_out/sw/t.bin > gpurun_out/sw/t.txt
+for cfg in "--no-giant" "--no-giant --bundle-budget 4096" "--no-giant --bundle-budget 256"; do
+  n=$(echo $cfg | tr -d ' -')
+  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu $cfg > gpurun_out/sw/$n.json 2> gpurun_out/sw/$n.err
+done
