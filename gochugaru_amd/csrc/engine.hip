@@ -187,28 +187,48 @@ __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t ob
   c.queries[q].last_alive = c.level + 1;  // benign race: every writer stores the same value
 }
 
+// Device reads through the pointers a DevCSR holds. Those pointers are loaded from memory, so
+// the compiler cannot tell they point at HBM and would emit flat instructions, whose waits also
+// drain every outstanding LDS operation (and vice versa); the explicit global address space keeps
+// them global_load_* (vmcnt only).
+#define GCK_GLOBAL __attribute__((address_space(1)))
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+template <class T>
+__device__ __forceinline__ const GCK_GLOBAL T* gptr(const T* p) {
+  return (const GCK_GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ GCK_GLOBAL T* gptr_w(T* p) {
+  return (GCK_GLOBAL T*)p;
+}
+__device__ __forceinline__ uint32_t csr_off(const DevCSR& r, uint32_t i) { return gptr(r.off)[i]; }
+__device__ __forceinline__ uint32_t csr_nbr(const DevCSR& r, uint32_t p) { return gptr(r.nbr)[p]; }
+__device__ __forceinline__ uint32_t csr_cav(const DevCSR& r, uint32_t p) { return gptr(r.cav)[p]; }
+__device__ __forceinline__ int64_t csr_exp(const DevCSR& r, uint32_t p) { return gptr(r.exp_us)[p]; }
+
 // lower_bound of `sid` in the CSR row of `obj`; returns the position or kNone.
 __device__ __forceinline__ uint32_t row_find(const DevCSR& r, uint32_t obj, uint32_t sid,
                                              uint32_t& probes) {
   if (obj >= r.n_rows) return kNone;
-  uint32_t lo = r.off[obj], hi = r.off[obj + 1];
+  uint32_t lo = csr_off(r, obj), hi = csr_off(r, obj + 1);
   const uint32_t end = hi;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
     ++probes;
-    if (r.nbr[mid] < sid) lo = mid + 1;
+    if (csr_nbr(r, mid) < sid) lo = mid + 1;
     else hi = mid;
   }
   if (lo < end) {
     if (hi == end) ++probes;  // the final equality read when the loop never touched lo
-    if (r.nbr[lo] == sid) return lo;
+    if (csr_nbr(r, lo) == sid) return lo;
   }
   return kNone;
 }
 
 __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t now_us) {
   if (!r.is_ext) return true;
-  int64_t x = r.exp_us[pos];
+  int64_t x = csr_exp(r, pos);
   return x == 0 || x > now_us;
 }
 
@@ -218,8 +238,8 @@ constexpr int kBucketKeys = 8;  // 8 x u64 = 64 B
 
 __device__ __forceinline__ uint32_t bucket_probe(const unsigned long long* tab, uint32_t b,
                                                  unsigned long long key) {
-  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(tab + (size_t)b * kBucketKeys);
-  const ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+  const GCK_GLOBAL u64x2* p = (const GCK_GLOBAL u64x2*)(tab + (size_t)b * kBucketKeys);
+  const u64x2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
   const bool hit = a0.x == key || a0.y == key || a1.x == key || a1.y == key || a2.x == key ||
                    a2.y == key || a3.x == key || a3.y == key;
   const bool empty = a0.x == kEmptyKey || a0.y == kEmptyKey || a1.x == kEmptyKey || a1.y == kEmptyKey ||
@@ -269,13 +289,13 @@ __device__ __forceinline__ uint32_t member_test(const DevCSR& r, uint32_t obj, u
   uint32_t best = 0;
   if (direct) {
     const uint32_t p = row_find(r, obj, sid, probes);
-    if (p != kNone && visible(r, p, now_us)) best = (r.is_ext && r.cav[p] != 0) ? 2u : 1u;
+    if (p != kNone && visible(r, p, now_us)) best = (r.is_ext && csr_cav(r, p) != 0) ? 2u : 1u;
   }
   if (wild && best != 1) {
-    const uint32_t b = r.off[obj], en = r.off[obj + 1];
+    const uint32_t b = csr_off(r, obj), en = csr_off(r, obj + 1);
     ++probes;
-    if (en > b && r.nbr[en - 1] == kWildcard && visible(r, en - 1, now_us)) {
-      const uint32_t m = (r.is_ext && r.cav[en - 1] != 0) ? 2u : 1u;
+    if (en > b && csr_nbr(r, en - 1) == kWildcard && visible(r, en - 1, now_us)) {
+      const uint32_t m = (r.is_ext && csr_cav(r, en - 1) != 0) ? 2u : 1u;
       if (best == 0 || m == 1) best = m;
     }
   }
@@ -289,7 +309,7 @@ __device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_
   const DevCSR& r = c.csrs[csr];
   if (obj >= r.n_rows) return;
   ++rows;
-  uint32_t b = r.off[obj], e = r.off[obj + 1];
+  uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
   if (e == b) return;
   unsigned long long packed =
       atomicAdd(&c.ctr->seg_ctr, (1ull << 40) | (unsigned long long)(e - b));
@@ -327,7 +347,7 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         const DevCSR& r = c.csrs[ci];
         if (obj >= r.n_rows) continue;
         ++rows;
-        uint32_t b = r.off[obj], e = r.off[obj + 1];
+        uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
           if (it.target == kNoNode) missing = true;
@@ -382,11 +402,11 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         if (ci == kNone) continue;
         const DevCSR& r = c.csrs[ci];
         if (obj >= r.n_rows) continue;
-        uint32_t b = r.off[obj], e = r.off[obj + 1];
+        uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
-          uint32_t cav = r.is_ext ? (r.cav[p] != 0) : 0u;
-          push_entry(c, q0 + k, r.nbr[p], it.target, depth + 1, cav);
+          uint32_t cav = r.is_ext ? (csr_cav(r, p) != 0) : 0u;
+          push_entry(c, q0 + k, csr_nbr(r, p), it.target, depth + 1, cav);
           ++k;
         }
       }
@@ -557,13 +577,13 @@ __global__ void __launch_bounds__(kBlock) k_edges(Ctx c) {
     if (qflags(&c.queries[s.q]) & QF_DONE) continue;
     const DevCSR& r = c.csrs[s.csr];
     const uint32_t p = s.begin + (uint32_t)off;
-    const uint32_t x = r.nbr[p];
+    const uint32_t x = csr_nbr(r, p);
     ++done_edges;
     uint32_t cond = s.cond;
     if (r.is_ext) {
       ++ext_edges;
       if (!visible(r, p, c.now_us)) continue;
-      cond |= (r.cav[p] != 0);
+      cond |= (csr_cav(r, p) != 0);
     }
     if (x == kWildcard) continue;
     push_entry(c, s.q, x, s.target, s.depth, cond);
