@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--giant-slots", type=int, default=0)
     ap.add_argument("--wide-only", action="store_true")
     ap.add_argument("--no-giant", action="store_true", help="deferred checks go to the grid-wide path")
+    ap.add_argument("--no-bidir", action="store_true", help="forward-only search (no bidirectional checks)")
+    ap.add_argument("--bidir-both", type=int, default=0, help="expand both sides while <= this many entries")
     return ap.parse_args()
 
 
@@ -84,7 +86,7 @@ def main():
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
                  bundle_budget=args.bundle_budget, giant_slots=args.giant_slots,
-                 giant_stage=not args.no_giant)
+                 giant_stage=not args.no_giant, bidir=not args.no_bidir, bidir_both=args.bidir_both)
     eng.load_schema(synth.SCHEMA)
     assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
     assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW

@@ -51,6 +51,8 @@ struct DeviceSnapshot {
   DevCSR* csrs = nullptr;
   uint32_t* type_counts = nullptr;
   uint32_t n_nodes = 0, n_items = 0, n_csrs = 0, n_types = 0, n_rels = 0;
+  uint32_t n_fwd = 0;      // forward nodes; [n_fwd, n_nodes) is the reverse program (bidir.inc)
+  bool has_bidir = false;  // some forward node is NF_BIDIR
   uint32_t node_bits = 1, q_bits = 1;
   uint64_t bytes = 0;
 };
@@ -103,6 +105,7 @@ struct Ctx {
   const uint32_t* type_counts;
   uint32_t n_types, n_rels;
   uint32_t n_nodes, n_items, n_csrs;
+  uint32_t n_fwd;  // forward nodes (reverse-program nodes follow)
   DevCheck* checks;
   DevQuery* queries;
   DevJoin* joins;
@@ -863,6 +866,8 @@ void device_free(Engine& e) {
 
 uint64_t device_bytes(const Engine& e) { return e.dev ? e.dev->bytes : 0; }
 
+#include "bidir.inc"
+
 void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
@@ -870,6 +875,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
   auto* ds = new DeviceSnapshot();
   try {
     std::vector<DevCSR> table;
+    std::vector<CsrInfo> info;
     unsigned* wild_flag = dalloc<unsigned>(ds->allocs, 1);
     for (HostCSR& h : csrs) {
       DevCSR d{};
@@ -916,6 +922,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
         d.has_wild = hw ? 1 : 0;
       }
       table.push_back(d);
+      info.push_back({ne, h.stype});
     }
     HIP_OK(hipDeviceSynchronize());
     // link the node program to the CSR table
@@ -931,16 +938,18 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
         }
       }
     }
-    ds->n_nodes = (uint32_t)sc.nodes.size();
+    std::vector<DevNode> nodes = sc.nodes;
+    build_bidir(e, *ds, nodes, items, table, info);
+    ds->n_nodes = (uint32_t)nodes.size();
     ds->n_items = (uint32_t)items.size();
     ds->n_csrs = (uint32_t)table.size();
     ds->n_types = (uint32_t)sc.types.size();
     ds->n_rels = (uint32_t)sc.rels.size();
-    ds->nodes = dalloc<DevNode>(ds->allocs, sc.nodes.size(), &ds->bytes);
+    ds->nodes = dalloc<DevNode>(ds->allocs, nodes.size(), &ds->bytes);
     ds->items = dalloc<DevItem>(ds->allocs, items.size(), &ds->bytes);
     ds->csrs = dalloc<DevCSR>(ds->allocs, table.size(), &ds->bytes);
     ds->type_counts = dalloc<uint32_t>(ds->allocs, sc.types.size(), &ds->bytes);
-    HIP_OK(hipMemcpy(ds->nodes, sc.nodes.data(), sc.nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(ds->nodes, nodes.data(), nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
     if (!items.empty())
       HIP_OK(hipMemcpy(ds->items, items.data(), items.size() * sizeof(DevItem), hipMemcpyHostToDevice));
     if (!table.empty())
@@ -1055,6 +1064,7 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.n_nodes = ds.n_nodes;
   c.n_items = ds.n_items;
   c.n_csrs = ds.n_csrs;
+  c.n_fwd = ds.n_fwd;
   c.checks = w.checks;
   c.queries = w.queries;
   c.joins = w.joins;
@@ -1190,6 +1200,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   if (dbg_on && !dbg) HIP_OK(hipMalloc(&dbg, dbg_words * 4));
   a.dbg = dbg_on ? dbg : nullptr;
   a.budget = w.b_budget;
+  a.both = e.cfg.bidir_both ? e.cfg.bidir_both : 64;
   a.idx = nullptr;
   a.n_dev = nullptr;
   // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
@@ -1230,19 +1241,25 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   const size_t prog_bytes = (size_t)c.n_csrs * sizeof(DevCSR) + (size_t)c.n_nodes * sizeof(DevNode) +
                             (size_t)c.n_items * sizeof(DevItem);
   const bool prog_lds = prog_bytes <= (size_t)kProgBytes;
-  if (prog_lds)
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  // bidirectional instantiation only when the snapshot has an eligible permission (bidir.inc)
+  const bool bd = e.dev->has_bidir;
+  if (prog_lds && bd)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else if (prog_lds)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else if (bd)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
   else
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
   HIP_OK(hipGetLastError());
   if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
   const bool giant = !(e.cfg.flags & GCK_FLAG_NO_GIANT);
   if (giant) {
     if (prog_lds)
-      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, true>), dim3(w.g_slots),
+      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, true, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
     else
-      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, false>), dim3(w.g_slots),
+      hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, false, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
     HIP_OK(hipGetLastError());
   }
@@ -1268,6 +1285,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   e.stats.membership_probes += h.probes;
   e.stats.edges_enumerated += h.edges;
   e.stats.ext_edges += h.ext_edges;
+  e.stats.bidir_checks += h.bidir;
   e.stats.queries += n;
   e.stats.batches++;
   if (dbg_on) {

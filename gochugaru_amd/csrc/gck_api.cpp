@@ -62,6 +62,10 @@ static Schema& need_schema(Engine& e) {
 
 extern "C" {
 
+static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
+static_assert(sizeof(gck_stats) == 176, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
+static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32, "item/tuple layout");
+
 int gck_abi_version(void) { return GCK_ABI_VERSION; }
 
 const char* gck_last_error(void) { return g_last_error.c_str(); }

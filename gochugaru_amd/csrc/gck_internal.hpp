@@ -29,7 +29,8 @@ enum NodeKind : uint8_t {
 };
 
 enum NodeFlags : uint8_t {
-  NF_REAL = 1,  // a schema relation/permission: the identity filter applies
+  NF_REAL = 1,   // a schema relation/permission: the identity filter applies
+  NF_BIDIR = 2,  // a forward node whose checks may run bidirectionally (engine.hip build_bidir)
 };
 
 enum ItemKind : uint8_t {
@@ -46,7 +47,11 @@ struct DevNode {
   uint8_t flags;
   uint32_t first;  // first DevItem
   uint32_t count;  // number of DevItems
-  uint32_t pad;
+  // NF_BIDIR roots only, over forward nodes t < 32: bit t of `cmask` = t is in this node's
+  // closure; bit t of `lmask` = t is reached from this node through computed usersets only,
+  // so a vertex (o, t) of a check's closure has o == the check's resource
+  uint32_t cmask;
+  uint32_t lmask;
 };
 
 struct DevItem {
@@ -156,6 +161,7 @@ struct DevCounters {  // device-side counters, reset per level where noted
   unsigned long long edges;
   unsigned long long ext_edges;
   unsigned long long expanded;
+  unsigned long long bidir;         // checks evaluated bidirectionally
 };
 
 }  // namespace gck

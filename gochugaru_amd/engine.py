@@ -48,6 +48,7 @@ FLAG_PROFILE = 1
 FLAG_NO_BUNDLE = 2
 FLAG_NO_MHASH = 4
 FLAG_NO_GIANT = 8
+FLAG_NO_BIDIR = 16
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -88,7 +89,8 @@ class _Config(C.Structure):
                 ("bundle_frontier", C.c_uint32), ("bundle_visited", C.c_uint32),
                 ("bundle_waves_per_cu", C.c_uint32), ("bundle_budget", C.c_uint32),
                 ("giant_frontier", C.c_uint32), ("giant_visited", C.c_uint32),
-                ("giant_slots", C.c_uint32)]
+                ("giant_slots", C.c_uint32), ("bidir_both", C.c_uint32),
+                ("reserved0", C.c_uint32)]
 
 
 class _Consistency(C.Structure):
@@ -104,7 +106,8 @@ class _Stats(C.Structure):
                 ("resolve_ms", C.c_double), ("expand_launches", C.c_uint64),
                 ("edges_launches", C.c_uint64), ("bundle_ms", C.c_double),
                 ("bundle_launches", C.c_uint64), ("deferred", C.c_uint64),
-                ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64)]
+                ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64),
+                ("bidir_checks", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -190,14 +193,16 @@ class Engine:
                  wide_only: bool = False, bundle_checks: int = 0, bundle_frontier: int = 0,
                  bundle_visited: int = 0, bundle_waves_per_cu: int = 0,
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
-                 giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True):
+                 giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
+                 bidir: bool = True, bidir_both: int = 0):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
-                 | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT))
+                 | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
+                 | (0 if bidir else FLAG_NO_BIDIR))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,
-                      giant_visited, giant_slots)
+                      giant_visited, giant_slots, bidir_both, 0)
         h = _P()
         _check(lib.gck_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 1
+#define GCK_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -83,6 +83,7 @@ extern "C" {
 #define GCK_FLAG_NO_BUNDLE 2u    /* gck_config.flags: grid-wide level-synchronous path only */
 #define GCK_FLAG_NO_MHASH 4u     /* gck_config.flags: no hashed membership index (binary search) */
 #define GCK_FLAG_NO_GIANT 8u     /* gck_config.flags: deferred checks skip the workgroup-bundle stage */
+#define GCK_FLAG_NO_BIDIR 16u    /* gck_config.flags: forward-only search (no bidirectional checks) */
 
 typedef struct gck_engine gck_engine;
 
@@ -95,7 +96,7 @@ typedef struct gck_config {
   uint64_t frontier_capacity;  /* entries per frontier buffer; 0 = auto */
   uint64_t segment_capacity;   /* row segments per level; 0 = auto */
   uint64_t query_capacity;     /* queries per batch (checks + sub-queries of joins); 0 = auto */
-  uint32_t bundle_checks;      /* checks per wavefront bundle (1..64); 0 = 16 */
+  uint32_t bundle_checks;      /* checks per wavefront bundle (1..32); 0 = 16 */
   uint32_t bundle_frontier;    /* frontier entries per wavefront; 0 = 4096 */
   uint32_t bundle_visited;     /* visited slots per wavefront (power of 2); 0 = 16384 */
   uint32_t bundle_waves_per_cu;/* resident wavefronts per CU for the bundle kernel; 0 = 16 */
@@ -104,6 +105,9 @@ typedef struct gck_config {
   uint32_t giant_frontier;     /* frontier entries per 16-wave workgroup bundle; 0 = 65536 */
   uint32_t giant_visited;      /* visited slots per workgroup bundle (power of 2); 0 = 262144 */
   uint32_t giant_slots;        /* resident workgroup bundles; 0 = one per CU */
+  uint32_t bidir_both;         /* bidirectional checks expand both sides while their two
+                                  frontiers hold at most this many entries; 0 = 64 */
+  uint32_t reserved0;
 } gck_config;
 
 /* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
@@ -157,6 +161,7 @@ typedef struct gck_stats {
   uint64_t deferred;           /* checks handed from wavefront bundles to workgroup bundles */
   double giant_ms;             /* GCK_FLAG_PROFILE: summed workgroup-bundle kernel time */
   uint64_t deferred_wide;      /* checks handed from workgroup bundles to the grid-wide path */
+  uint64_t bidir_checks;       /* checks evaluated bidirectionally (forward + reverse frontier) */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

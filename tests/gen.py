@@ -244,5 +244,54 @@ def nested(seed, n_users=200, n_groups=120, layers=8, n_docs=80):
     return NESTED, t, checks
 
 
-FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested}
+def gdocs_deep(seed, n_users=80, n_groups=40, n_folders=40, n_docs=60):
+    """GDocs schema without wildcards (every doc/folder permission is a plain union, so checks
+    run bidirectionally) and long group / folder chains; a fifth of the checks have a userset
+    subject."""
+    rng = random.Random(seed)
+    t = []
+    for g in range(n_groups):
+        for _ in range(rng.randint(0, 3)):
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}")
+        if g + 1 < n_groups and rng.random() < 0.7:  # a chain with occasional branches
+            t.append(f"group:g{g}#member@group:g{g + 1 + (rng.random() < 0.2)}#member".replace(f"g{n_groups}#", f"g{n_groups - 1}#"))
+    for f in range(n_folders):
+        if f > 0 and rng.random() < 0.9:
+            t.append(f"folder:f{f}#parent@folder:f{max(0, f - 1 - _pick(rng, 2))}")
+        for rel in ("viewer", "editor"):
+            for _ in range(rng.randint(0, 1)):
+                if rng.random() < 0.4:
+                    t.append(f"folder:f{f}#{rel}@user:u{_pick(rng, n_users)}")
+                else:
+                    t.append(f"folder:f{f}#{rel}@group:g{_pick(rng, n_groups)}#member")
+    for d in range(n_docs):
+        if rng.random() < 0.9:
+            t.append(f"doc:d{d}#parent@folder:f{_pick(rng, n_folders)}")
+        if rng.random() < 0.3:
+            t.append(f"doc:d{d}#owner@user:u{_pick(rng, n_users)}")
+        for rel in ("viewer", "editor"):
+            if rng.random() < 0.4:
+                if rng.random() < 0.5:
+                    t.append(f"doc:d{d}#{rel}@user:u{_pick(rng, n_users)}")
+                else:
+                    t.append(f"doc:d{d}#{rel}@group:g{_pick(rng, n_groups)}#member")
+    t = sorted(set(x for x in t if "#member@group:g" not in x or x.split("#")[0] != x.split("@")[1].split("#")[0]))
+    checks = []
+    for _ in range(400):
+        x = rng.random()
+        if x < 0.5:
+            checks.append(f"doc:d{_pick(rng, n_docs + 2)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users + 2)}")
+        elif x < 0.65:
+            checks.append(f"folder:f{_pick(rng, n_folders)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users)}")
+        elif x < 0.8:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@user:u{_pick(rng, n_users)}")
+        elif x < 0.9:
+            checks.append(f"doc:d{_pick(rng, n_docs)}#view@group:g{_pick(rng, n_groups)}#member")
+        else:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@group:g{_pick(rng, n_groups)}#member")
+    return GDOCS, t, checks
+
+
+FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested,
+            "gdocs_deep": gdocs_deep}
 NOW_US = 1759449600 * 1_000_000  # 2025-10-03T00:00:00Z

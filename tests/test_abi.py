@@ -34,8 +34,9 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert E.ITEM_DTYPE.itemsize == 20
     assert E.TUPLE_DTYPE.itemsize == 32
-    assert C.sizeof(E._Config) == 80
-    assert E.load_library().gck_abi_version() == 1
+    assert C.sizeof(E._Config) == 88
+    assert C.sizeof(E._Stats) == 176
+    assert E.load_library().gck_abi_version() == 2
 
 
 @pytest.fixture()

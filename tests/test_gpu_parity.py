@@ -165,6 +165,13 @@ PATHS = {
     # binary-search membership instead of the hashed index, both paths
     "nohash": {"membership_hash": False},
     "nohash-wide": {"membership_hash": False, "wide_only": True},
+    # forward-only wave bundles (no bidirectional checks)
+    "nobidir": {"bidir": False},
+    # bidirectional checks always expanding only the smaller side (most carrying) ...
+    "bidir-one": {"bidir_both": 1},
+    # ... or always both sides; and bidirectional checks deferred to the later stages
+    "bidir-all": {"bidir_both": 1 << 30},
+    "bidir-deferred": {"bundle_budget": 6, "bundle_frontier": 16, "bundle_visited": 64},
 }
 
 
@@ -183,6 +190,10 @@ def test_random_parity(family, seed, path):
         assert e.stats()["deferred"] > 0
     if path == "bundle":
         assert e.stats()["deferred"] == 0
+    if path == "bundle" and family in ("nested", "gdocs_deep"):
+        assert e.stats()["bidir_checks"] > 0
+    if path in ("nobidir", "wide") or family == "caveated":
+        assert e.stats()["bidir_checks"] == 0
     e.close()
 
 
