@@ -866,6 +866,33 @@ void device_free(Engine& e) {
 
 uint64_t device_bytes(const Engine& e) { return e.dev ? e.dev->bytes : 0; }
 
+// Membership index of a plain CSR (d.off / d.nbr on the device): sets d.mhash, d.mmask and
+// d.has_wild.
+static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
+  const uint64_t slots = 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne));
+  if (slots / kBucketKeys > (1ull << 32)) throw Error(GCK_E_CAPACITY, "membership index too large");
+  unsigned long long* tab = dalloc<unsigned long long>(ds.allocs, slots, &ds.bytes);
+  std::vector<void*> tmp;
+  unsigned* wild_flag = dalloc<unsigned>(tmp, 1);
+  unsigned hw = 0;
+  try {
+    HIP_OK(hipMemset(tab, 0xFF, slots * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(wild_flag, 0, sizeof(unsigned)));
+    const uint64_t blocks = (ne + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_build_mhash, dim3((uint32_t)blocks), dim3(kBlock), 0, 0, d.off, d.nbr, d.n_rows,
+                       (unsigned long long)ne, tab, (unsigned long long)(slots / kBucketKeys - 1), wild_flag);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpy(&hw, wild_flag, sizeof(unsigned), hipMemcpyDeviceToHost));
+  } catch (...) {
+    free_list(tmp);
+    throw;
+  }
+  free_list(tmp);
+  d.mhash = tab;
+  d.mmask = slots / kBucketKeys - 1;
+  d.has_wild = hw ? 1 : 0;
+}
+
 #include "bidir.inc"
 
 void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
@@ -876,7 +903,6 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
   try {
     std::vector<DevCSR> table;
     std::vector<CsrInfo> info;
-    unsigned* wild_flag = dalloc<unsigned>(ds->allocs, 1);
     for (HostCSR& h : csrs) {
       DevCSR d{};
       d.n_rows = h.n_rows;
@@ -905,22 +931,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
-      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
-        const uint64_t slots = 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne));
-        if (slots / kBucketKeys > (1ull << 32)) throw Error(GCK_E_CAPACITY, "membership index too large");
-        unsigned long long* tab = dalloc<unsigned long long>(ds->allocs, slots, &ds->bytes);
-        HIP_OK(hipMemset(tab, 0xFF, slots * sizeof(unsigned long long)));
-        HIP_OK(hipMemset(wild_flag, 0, sizeof(unsigned)));
-        const uint64_t blocks = (ne + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_build_mhash, dim3((uint32_t)blocks), dim3(kBlock), 0, 0, off, nbr, h.n_rows,
-                           (unsigned long long)ne, tab, (unsigned long long)(slots / kBucketKeys - 1), wild_flag);
-        HIP_OK(hipGetLastError());
-        unsigned hw = 0;
-        HIP_OK(hipMemcpy(&hw, wild_flag, sizeof(unsigned), hipMemcpyDeviceToHost));
-        d.mhash = tab;
-        d.mmask = slots / kBucketKeys - 1;
-        d.has_wild = hw ? 1 : 0;
-      }
+      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) build_mhash(*ds, d, ne);
       table.push_back(d);
       info.push_back({ne, h.stype});
     }

@@ -39,6 +39,10 @@ enum ItemKind : uint8_t {
   IT_ARROW = 2,     // tuple-to-userset over one tupleset kind: csr_*, target node (+1 depth)
   IT_SUB = 3,       // nested join node evaluated inline (no dispatch)
   IT_OPERAND = 4,   // join operand: target node, `dispatch` says whether depth advances
+  IT_REV = 5,       // reverse program (bidir.inc): in-edge of a userset / arrow / direct item.
+                    // csr_plain = the transposed CSR (subject -> objects), csr_ext = the forward
+                    // CSR (probed instead when the target is local to the check's root), target
+                    // = rev(node of the forward item)
 };
 
 struct DevNode {
@@ -50,8 +54,12 @@ struct DevNode {
   // NF_BIDIR roots only, over forward nodes t < 32: bit t of `cmask` = t is in this node's
   // closure; bit t of `lmask` = t is reached from this node through computed usersets only,
   // so a vertex (o, t) of a check's closure has o == the check's resource
+  // Reverse nodes: bit t of `cmask` = an in-edge of this node enters forward node t and can be
+  // probed on the forward CSR; bit 31 = it has another kind of item.
   uint32_t cmask;
   uint32_t lmask;
+  uint16_t canon;  // visited-key node id: the node itself; rev'(t) -> rev(t) (bidir.inc)
+  uint16_t lcsr;   // NF_BIDIR roots: the forward CSR whose row R each check caches (0xFFFF: none)
 };
 
 struct DevItem {

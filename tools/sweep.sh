@@ -1,9 +1,11 @@
+# Parameter sweep of the bench (no oracle, no CPU baseline): one JSON line per config.
+# Usage on the GPU box: bash tools/sweep.sh <out dir> "<flags 1>" "<flags 2>" ...
 set -e
-mkdir -p gpurun_out/sw
-rm -f gpurun_out/sw/t.bin
-GCK_DEBUG_TIMING=gpurun_out/sw/t timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/sw/t.json 2> gpurun_out/sw/t.err
-python tests/analyze_timing.py gpurun_out/sw/t.bin > gpurun_out/sw/t.txt
-for cfg in "--no-giant" "--no-giant --bundle-budget 4096" "--no-giant --bundle-budget 256"; do
-  n=$(echo $cfg | tr -d ' -')
-  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu $cfg > gpurun_out/sw/$n.json 2> gpurun_out/sw/$n.err
+OUT=$1; shift
+mkdir -p "$OUT"
+i=0
+for cfg in "$@"; do
+  i=$((i+1))
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-oracle $cfg > "$OUT/s$i.json" 2> "$OUT/s$i.err"
+  echo "$cfg :: $(python -c "import json,sys; d=json.load(open('$OUT/s$i.json')); print(d['value'], d['engine'])")"
 done

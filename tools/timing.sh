@@ -1,6 +1,11 @@
+# Per-bundle phase timing (make TIMING=1 build on the box) of one bench configuration.
+# Usage on the GPU box: bash tools/timing.sh <out dir> [bench flags]
 set -e
-mkdir -p gpurun_out/sw
+OUT=$1; shift
+mkdir -p "$OUT"
 touch gochugaru_amd/csrc/bundle.inc && make -C gochugaru_amd/csrc TIMING=1 > /dev/null
-rm -f gpurun_out/sw/t.bin
-GCK_DEBUG_TIMING=gpurun_out/sw/t timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu "$@" > gpurun_out/sw/t.json 2> gpurun_out/sw/t.err
-python tests/analyze_timing.py gpurun_out/sw/t.bin > gpurun_out/sw/t.txt
+rm -f "$OUT/t.bin"
+GCK_DEBUG_TIMING=$OUT/t timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --no-oracle "$@" > "$OUT/t.json" 2> "$OUT/t.err"
+python tests/analyze_timing.py "$OUT/t.bin" > "$OUT/t.txt"
+cat "$OUT/t.txt"
+touch gochugaru_amd/csrc/bundle.inc && make -C gochugaru_amd/csrc > /dev/null
