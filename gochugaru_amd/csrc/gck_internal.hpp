@@ -31,6 +31,7 @@ enum NodeKind : uint8_t {
 enum NodeFlags : uint8_t {
   NF_REAL = 1,   // a schema relation/permission: the identity filter applies
   NF_BIDIR = 2,  // a forward node whose checks may run bidirectionally (engine.hip build_bidir)
+  NF_JUMP = 4,   // a reverse node whose first item is an ancestor-closure jump (bidir.inc)
 };
 
 enum ItemKind : uint8_t {
