@@ -23,6 +23,7 @@ import time
 from typing import Iterable, Iterator, List, Optional, Tuple
 
 from . import consistency as _cs
+from . import rel as _rel
 from .consistency import Background, Context, Strategy
 from .engine import (CONSISTENCY_AT_LEAST, CONSISTENCY_FULL, CONSISTENCY_MIN_LATENCY,
                      CONSISTENCY_SNAPSHOT, GCK_E_DEVICE, GCK_E_REVISION, ITEM_ERROR_MESSAGES,
@@ -195,3 +196,18 @@ class Client:
         self.engine.load_schema(schema)
         lines = "\n".join(r.String() if hasattr(r, "String") else str(r) for r in relationships)
         self.engine.load_snapshot_text(revision, lines)
+
+    _UPDATE_OPS = {_rel.UpdateCreate: "CREATE", _rel.UpdateTouch: "TOUCH", _rel.UpdateDelete: "DELETE"}
+
+    def ApplyUpdates(self, revision: int, updates: Iterable) -> None:
+        """Fold one Watch response into the local snapshot: the ``rel.Update`` values that
+        ``UpdatesSinceRevision`` yields (client/client.go:370-413, rel/relationship.go:291-301)
+        up to the response's ChangesThrough revision (which gochugaru's iterator drops; the
+        caller passes it here). ``UpdateUnknown`` is rejected, as SpiceDB never sends it."""
+        lines = []
+        for u in updates:
+            op = self._UPDATE_OPS.get(u.UpdateType)
+            if op is None:
+                raise InvalidArgument(f"unknown update type {u.UpdateType!r}")
+            lines.append(op + " " + u.Relationship.String())
+        self.engine.apply_updates_text(revision, "\n".join(lines))

@@ -44,8 +44,29 @@ constexpr int kBlock = 256;
 constexpr unsigned long long kEmptyKey = ~0ull;
 constexpr uint32_t kResErr = 0xF;
 
+struct BaseCsr {  // a CSR of the snapshot itself: table[k] for k < base.size()
+  uint16_t rel, stype, srel;
+  bool ext;
+  uint64_t n_edges;
+  uint64_t mh_keys;  // keys + tombstones in its membership index (delta.inc)
+};
+
+struct Derived {  // a bidirectional structure and the base CSR it was built from (bidir.inc)
+  uint8_t kind;   // 0 = transposed CSR, 1 = ancestor closure
+  const uint32_t* src;
+  uint64_t src_edges;
+  DevCSR d;
+};
+
 struct DeviceSnapshot {
   std::vector<void*> allocs;
+  std::vector<BaseCsr> base;
+  std::vector<DevCSR> table;     // host copy of the device CSR table (base, then derived)
+  std::vector<Derived> derived;  // reused by the next snapshot when the source is unchanged
+  // dispatch-graph heights (bidir.inc): reused while the row-edge CSRs and the node set are
+  std::vector<const uint32_t*> h_src;
+  std::vector<char> h_used;
+  std::vector<uint32_t> hmax;
   DevNode* nodes = nullptr;
   DevItem* items = nullptr;
   DevCSR* csrs = nullptr;
@@ -895,11 +916,16 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 
 #include "bidir.inc"
 
+// Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
+// (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
+// derived structures of unchanged CSRs. Taken-over arrays join the new snapshot's allocation
+// list only on success, so a failure frees nothing the previous snapshot still owns.
 void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
   Schema& sc = *e.schema;
   auto* ds = new DeviceSnapshot();
+  std::vector<void*> adopted;
   try {
     std::vector<DevCSR> table;
     std::vector<CsrInfo> info;
@@ -908,6 +934,32 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       d.n_rows = h.n_rows;
       d.is_ext = h.ext ? 1 : 0;
       uint64_t ne = h.dev_off ? h.n_edges : h.nbr.size();
+      BaseCsr b{h.rel, h.stype, h.srel, h.ext, ne, 0};
+      if (h.adopt) {
+        d.off = h.dev_off;
+        d.nbr = h.dev_nbr;
+        d.cav = h.dev_cav;
+        d.exp_us = h.dev_exp;
+        for (const void* p : {(const void*)h.dev_off, (const void*)h.dev_nbr, (const void*)h.dev_cav,
+                              (const void*)h.dev_exp})
+          if (p) adopted.push_back(const_cast<void*>(p));
+        ds->bytes += ((size_t)h.n_rows + 1) * 4 + ne * (h.ext ? 16 : 4);
+        if (h.dev_mhash) {
+          d.mhash = h.dev_mhash;
+          d.mmask = h.mmask;
+          d.has_wild = h.has_wild;
+          b.mh_keys = h.mh_keys;
+          adopted.push_back(const_cast<unsigned long long*>(h.dev_mhash));
+          ds->bytes += (h.mmask + 1) * kBucketKeys * 8;
+        } else if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+          build_mhash(*ds, d, ne);
+          b.mh_keys = ne;
+        }
+        table.push_back(d);
+        info.push_back({ne, h.stype});
+        ds->base.push_back(b);
+        continue;
+      }
       uint32_t* off = dalloc<uint32_t>(ds->allocs, (size_t)h.n_rows + 1, &ds->bytes);
       uint32_t* nbr = dalloc<uint32_t>(ds->allocs, ne, &ds->bytes);
       if (h.dev_off) {
@@ -931,9 +983,13 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
-      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) build_mhash(*ds, d, ne);
+      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+        build_mhash(*ds, d, ne);
+        b.mh_keys = ne;
+      }
       table.push_back(d);
       info.push_back({ne, h.stype});
+      ds->base.push_back(b);
     }
     HIP_OK(hipDeviceSynchronize());
     // link the node program to the CSR table
@@ -950,7 +1006,10 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       }
     }
     std::vector<DevNode> nodes = sc.nodes;
-    build_bidir(e, *ds, nodes, items, table, info);
+    build_bidir(e, *ds, nodes, items, table, info, adopted);
+    for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
+      if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
+    ds->table = table;
     ds->n_nodes = (uint32_t)nodes.size();
     ds->n_items = (uint32_t)items.size();
     ds->n_csrs = (uint32_t)table.size();
@@ -975,6 +1034,17 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     free_list(ds->allocs);
     delete ds;
     throw;
+  }
+  if (!adopted.empty()) {
+    std::sort(adopted.begin(), adopted.end());
+    adopted.erase(std::unique(adopted.begin(), adopted.end()), adopted.end());
+    if (e.dev) {  // the previous snapshot no longer owns what was taken over
+      auto& old = e.dev->allocs;
+      old.erase(std::remove_if(old.begin(), old.end(),
+                               [&](void* p) { return std::binary_search(adopted.begin(), adopted.end(), p); }),
+                old.end());
+    }
+    ds->allocs.insert(ds->allocs.end(), adopted.begin(), adopted.end());
   }
   if (e.dev) {
     free_list(e.dev->allocs);
@@ -1390,5 +1460,7 @@ void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_u
   }
   e.stats.kernel_ms = ms;
 }
+
+#include "delta.inc"
 
 }  // namespace gck

@@ -107,6 +107,25 @@ struct HostCSR {
   const uint32_t* dev_off = nullptr;
   const uint32_t* dev_nbr = nullptr;
   uint64_t n_edges = 0;
+  // delta re-link (delta.inc): the snapshot takes these device arrays over without a copy
+  bool adopt = false;
+  const uint32_t* dev_cav = nullptr;
+  const int64_t* dev_exp = nullptr;
+  const unsigned long long* dev_mhash = nullptr;  // nullptr: build the index if the kind has one
+  unsigned long long mmask = 0;
+  uint8_t has_wild = 0;
+  uint64_t mh_keys = 0;  // keys + tombstones in dev_mhash
+};
+
+// The updates of one (relation, subject type, subject relation), last write per key
+// (snapshot.cpp group_updates).
+struct UpdateGroup {
+  uint16_t rel, stype, srel;
+  std::vector<unsigned long long> keys;  // (object << 32) | subject, ascending, unique
+  std::vector<uint8_t> upsert;           // 1 = CREATE / TOUCH, 0 = DELETE
+  std::vector<uint8_t> is_ext;           // the upsert carries a caveat or an expiration
+  std::vector<uint32_t> cav;             // caveat instance per key (0 = none)
+  std::vector<int64_t> exp_us;           // expiration per key (0 = never)
 };
 
 struct DeviceSnapshot;  // engine.hip
@@ -140,10 +159,14 @@ struct Engine {
 // snapshot.cpp
 void add_tuples_text(Engine& e, const char* text, size_t len);
 std::vector<HostCSR> build_csrs(Engine& e);
+// Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
+void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
+std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>& ups);
 
 // engine.hip
 int device_init(Engine& e);
 void device_upload(Engine& e, std::vector<HostCSR>& csrs);
+void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
 void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
                   uint8_t* d_perm, int32_t* d_err, void* stream);
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,

@@ -64,7 +64,7 @@ extern "C" {
 
 static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_stats) == 176, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
-static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32, "item/tuple layout");
+static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32 && sizeof(gck_update) == 40, "item/tuple/update layout");
 
 int gck_abi_version(void) { return GCK_ABI_VERSION; }
 
@@ -332,6 +332,48 @@ int gck_device_bytes(gck_engine* ge, uint64_t* out) {
     Engine& e = need(ge);
     REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
     *out = device_bytes(e);
+  });
+}
+
+// Watch batch: validated and grouped on the host first (nothing is applied if any update is
+// rejected), then merged on the device (delta.inc). A device failure loses the snapshot.
+static void apply_updates(Engine& e, uint64_t revision, const std::vector<gck_update>& ups) {
+  REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+  REQUIRE(revision > e.revision || (ups.empty() && revision == e.revision), GCK_E_REVISION,
+          "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
+              std::to_string(e.revision));
+  std::vector<UpdateGroup> groups = group_updates(e, ups);
+  if (!groups.empty()) {
+    try {
+      device_apply(e, groups);
+    } catch (...) {
+      e.committed = false;
+      throw;
+    }
+  }
+  e.revision = revision;
+}
+
+int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updates, size_t n) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(n == 0 || updates, GCK_E_INVALID_ARGUMENT, "null updates");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    apply_updates(e, revision, std::vector<gck_update>(updates, updates + n));
+  });
+}
+
+int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, size_t len) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    std::vector<gck_update> ups;
+    parse_updates_text(e, text, len, ups);
+    apply_updates(e, revision, ups);
   });
 }
 

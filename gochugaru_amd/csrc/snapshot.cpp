@@ -107,7 +107,8 @@ size_t json_end(const std::string& s, size_t i) {
 
 uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json);
 
-void stage_tuple(Engine& e, const gck_tuple& t) {
+// Schema and interner validation of one relationship (WriteRelationships would reject it).
+void validate_tuple(const Engine& e, const gck_tuple& t) {
   const Schema& sc = *e.schema;
   if (t.resource_type >= sc.types.size() || t.subject_type >= sc.types.size())
     throw Error(GCK_E_INVALID_ARGUMENT, "tuple references an unknown type");
@@ -133,6 +134,10 @@ void stage_tuple(Engine& e, const gck_tuple& t) {
     throw Error(GCK_E_INVALID_ARGUMENT, "tuple references an object id that was never interned");
   if (t.caveat >= e.caveat_instances.size())
     throw Error(GCK_E_INVALID_ARGUMENT, "unknown caveat instance id");
+}
+
+void stage_tuple(Engine& e, const gck_tuple& t) {
+  validate_tuple(e, t);
   StagedTuple s{};
   s.rel = t.relation;
   s.stype = t.subject_type;
@@ -145,9 +150,11 @@ void stage_tuple(Engine& e, const gck_tuple& t) {
   e.staged.push_back(s);
 }
 
-// One canonical line: type:id#rel@type:id[#rel][caveat[:{json}]][expiration:T]
-void add_tuples_text(Engine& e, const char* text, size_t len) {
-  const Schema& sc = *e.schema;
+namespace {
+
+// Splits text into trimmed lines, skipping blank lines and comments ('#', '//').
+template <class F>
+void for_each_line(const char* text, size_t len, F&& f) {
   size_t pos = 0;
   while (pos < len) {
     size_t nl = pos;
@@ -159,6 +166,15 @@ void add_tuples_text(Engine& e, const char* text, size_t len) {
     while (st < line.size() && (line[st] == ' ' || line[st] == '\t')) ++st;
     line = line.substr(st);
     if (line.empty() || line[0] == '#' || line.compare(0, 2, "//") == 0) continue;
+    f(line);
+  }
+}
+
+// One canonical line: type:id#rel@type:id[#rel][caveat[:{json}]][expiration:T]. Interns the
+// ids (creating them) and registers the caveat instance.
+gck_tuple parse_tuple_line(Engine& e, const std::string& line) {
+  const Schema& sc = *e.schema;
+  {
     auto bad = [&](const char* why) {
       return Error(GCK_E_INVALID_ARGUMENT, std::string(why) + ": '" + line + "'");
     };
@@ -232,8 +248,86 @@ void add_tuples_text(Engine& e, const char* text, size_t len) {
     t.subject_id = intern_one(e, (uint16_t)stt, sid);
     t.caveat = cav_name.empty() ? 0 : add_caveat_instance(e, cav_name, cav_json);
     t.expires_at_us = exp_us;
-    stage_tuple(e, t);
+    return t;
   }
+}
+
+}  // namespace
+
+void add_tuples_text(Engine& e, const char* text, size_t len) {
+  for_each_line(text, len, [&](const std::string& line) { stage_tuple(e, parse_tuple_line(e, line)); });
+}
+
+// Watch updates as text, one per line: "<OP> <relationship>", OP = CREATE | TOUCH | DELETE
+// (rel.UpdateType, rel/relationship.go:267-274; the OPERATION_ prefix of the v1 proto enum is
+// accepted too).
+void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out) {
+  for_each_line(text, len, [&](const std::string& line) {
+    size_t sp = line.find_first_of(" \t");
+    if (sp == std::string::npos) throw Error(GCK_E_INVALID_ARGUMENT, "update without a relationship: '" + line + "'");
+    std::string op = line.substr(0, sp);
+    if (op.compare(0, 10, "OPERATION_") == 0) op = op.substr(10);
+    gck_update u{};
+    if (op == "CREATE") u.op = GCK_UPDATE_CREATE;
+    else if (op == "TOUCH") u.op = GCK_UPDATE_TOUCH;
+    else if (op == "DELETE") u.op = GCK_UPDATE_DELETE;
+    else throw Error(GCK_E_INVALID_ARGUMENT, "unknown update operation '" + op + "'");
+    size_t st = line.find_first_not_of(" \t", sp);
+    u.tuple = parse_tuple_line(e, line.substr(st));
+    out.push_back(u);
+  });
+}
+
+// Validates the updates and groups them per (relation, subject type, subject relation); within a
+// group the last write per (object, subject) wins (the order of the Watch stream).
+std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>& ups) {
+  struct U {
+    uint16_t rel, stype, srel;
+    uint32_t obj, sid, cav;
+    int64_t exp_us;
+    uint32_t op;
+    size_t seq;
+  };
+  std::vector<U> v;
+  v.reserve(ups.size());
+  for (size_t i = 0; i < ups.size(); ++i) {
+    const gck_update& u = ups[i];
+    if (u.op != GCK_UPDATE_CREATE && u.op != GCK_UPDATE_TOUCH && u.op != GCK_UPDATE_DELETE)
+      throw Error(GCK_E_INVALID_ARGUMENT, "unknown update operation " + std::to_string(u.op));
+    validate_tuple(e, u.tuple);
+    const gck_tuple& t = u.tuple;
+    v.push_back({t.relation, t.subject_type, t.subject_relation, t.resource_id, t.subject_id, t.caveat,
+                 t.expires_at_us, u.op, i});
+  }
+  std::sort(v.begin(), v.end(), [](const U& a, const U& b) {
+    if (a.rel != b.rel) return a.rel < b.rel;
+    if (a.stype != b.stype) return a.stype < b.stype;
+    if (a.srel != b.srel) return a.srel < b.srel;
+    if (a.obj != b.obj) return a.obj < b.obj;
+    if (a.sid != b.sid) return a.sid < b.sid;
+    return a.seq < b.seq;
+  });
+  std::vector<UpdateGroup> out;
+  for (size_t i = 0; i < v.size(); ++i) {
+    const U& x = v[i];
+    if (i + 1 < v.size() && v[i + 1].rel == x.rel && v[i + 1].stype == x.stype && v[i + 1].srel == x.srel &&
+        v[i + 1].obj == x.obj && v[i + 1].sid == x.sid)
+      continue;  // a later write of the same relationship follows
+    if (out.empty() || out.back().rel != x.rel || out.back().stype != x.stype || out.back().srel != x.srel) {
+      out.emplace_back();
+      out.back().rel = x.rel;
+      out.back().stype = x.stype;
+      out.back().srel = x.srel;
+    }
+    UpdateGroup& g = out.back();
+    g.keys.push_back(((unsigned long long)x.obj << 32) | x.sid);
+    const bool up = x.op != GCK_UPDATE_DELETE;
+    g.upsert.push_back(up ? 1 : 0);
+    g.is_ext.push_back(up && (x.cav != 0 || x.exp_us != 0) ? 1 : 0);
+    g.cav.push_back(up ? x.cav : 0);
+    g.exp_us.push_back(up ? x.exp_us : 0);
+  }
+  return out;
 }
 
 std::vector<HostCSR> build_csrs(Engine& e) {

@@ -65,6 +65,10 @@ TUPLE_DTYPE = np.dtype({
     "itemsize": 32,
 })
 
+UPDATE_CREATE, UPDATE_DELETE, UPDATE_TOUCH = 1, 2, 3  # rel.UpdateType (rel/relationship.go:267-274)
+UPDATE_DTYPE = np.dtype({"names": ["op", "reserved", "tuple"], "formats": ["<u4", "<u4", TUPLE_DTYPE],
+                         "offsets": [0, 4, 8], "itemsize": 40})
+
 ITEM_ERROR_MESSAGES = {
     ITEM_ERR_MAX_DEPTH: "max depth exceeded: this usually indicates a recursive or too deep data dependency",
     ITEM_ERR_UNKNOWN_PERMISSION: "relation/permission not found",
@@ -139,6 +143,8 @@ _SIGS = {
     "gck_revision": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_tuple_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_device_bytes": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_apply_updates": (C.c_int, [_P, C.c_uint64, _P, C.c_size_t]),
+    "gck_apply_updates_text": (C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "gck_check_bulk": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.c_int64, _P, _P]),
     "gck_check_bulk_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -347,6 +353,18 @@ class Engine:
         out = C.c_uint64()
         _check(self._lib.gck_device_bytes(self._h, C.byref(out)))
         return out.value
+
+    # ---- Watch updates (Client.UpdatesSinceRevision, client/client.go:370-413) -------------
+    def apply_updates(self, revision: int, updates: np.ndarray):
+        """One batch of interned updates (UPDATE_DTYPE records, stream order) -> `revision`."""
+        updates = np.ascontiguousarray(updates, dtype=UPDATE_DTYPE)
+        _check(self._lib.gck_apply_updates(self._h, revision, updates.ctypes.data if len(updates) else None,
+                                           len(updates)))
+
+    def apply_updates_text(self, revision: int, text: str):
+        """One batch as text: "<CREATE|TOUCH|DELETE> <rel.Relationship.String>" per line."""
+        b = text.encode()
+        _check(self._lib.gck_apply_updates_text(self._h, revision, b, len(b)))
 
     # ---- checks --------------------------------------------------------------------------
     def check_bulk(self, items: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY,

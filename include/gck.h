@@ -18,6 +18,9 @@
  *   gck_intern
  *       replaces the per-item string handling of Client.Check's item loop
  *       (client/client.go:242-259) with batched string -> dense u32 interning.
+ *   gck_apply_updates / gck_apply_updates_text
+ *       consume the rel.Update stream of Client.UpdatesSinceRevision (client/client.go:370-413,
+ *       rel.UpdateFromV1Proto rel/relationship.go:296-301) and keep the snapshot current.
  *   gck_revision / gck_check_bulk's consistency argument
  *       honour consistency.Strategy (consistency/consistency.go:15-77) as sent in
  *       CheckBulkPermissionsRequest.Consistency (client/client.go:263).
@@ -37,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 2
+#define GCK_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -133,6 +136,16 @@ typedef struct gck_tuple {
   int64_t expires_at_us;       /* unix microseconds; 0 = never */
 } gck_tuple;                   /* 32 bytes */
 
+/* One Watch update: rel.Update (rel/relationship.go:291-301), operation = rel.UpdateType. */
+#define GCK_UPDATE_CREATE 1u   /* rel.UpdateCreate (applied as an upsert) */
+#define GCK_UPDATE_DELETE 2u   /* rel.UpdateDelete */
+#define GCK_UPDATE_TOUCH 3u    /* rel.UpdateTouch */
+typedef struct gck_update {
+  uint32_t op;                 /* GCK_UPDATE_* */
+  uint32_t reserved;
+  gck_tuple tuple;
+} gck_update;                  /* 40 bytes */
+
 typedef struct gck_consistency {
   int32_t requirement;         /* GCK_CONSISTENCY_* */
   uint32_t reserved;
@@ -205,6 +218,18 @@ int gck_revision(gck_engine* e, uint64_t* out);
 int gck_tuple_count(gck_engine* e, uint64_t* out);
 /* Bytes resident in HBM for the snapshot (CSR + tables). */
 int gck_device_bytes(gck_engine* e, uint64_t* out);
+
+/* ---- Watch (Client.UpdatesSinceRevision, client/client.go:370-413) ------------------- */
+/* Applies one batch of updates (a Watch response, in stream order) to the committed snapshot
+ * and moves it to `revision` (the response's ChangesThrough token, decoded), which must be
+ * newer than the current one; an empty batch may also re-state the current revision. The merge
+ * runs on the device. Errors: GCK_E_REVISION (stale revision), GCK_E_INVALID_ARGUMENT (unknown
+ * operation / relationship the schema rejects; nothing applied), GCK_E_STATE (no snapshot).
+ * A device failure during the merge leaves no snapshot (GCK_E_STATE until the next commit). */
+int gck_apply_updates(gck_engine* e, uint64_t revision, const gck_update* updates, size_t n);
+/* Text form: one "<OP> <relationship>" per line, OP = CREATE | TOUCH | DELETE and the
+ * relationship in rel.Relationship.String form (rel/relationship.go:51-90). */
+int gck_apply_updates_text(gck_engine* e, uint64_t revision, const char* text, size_t len);
 
 /* ---- checks (CheckBulkPermissions, client/client.go:261-283) -------------------------- */
 /* Host buffers: items[n] in, out_perm[n] (GCK_PERM_*), out_err[n] (GCK_ITEM_*) out.

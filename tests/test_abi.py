@@ -34,9 +34,10 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert E.ITEM_DTYPE.itemsize == 20
     assert E.TUPLE_DTYPE.itemsize == 32
+    assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
     assert C.sizeof(E._Stats) == 176
-    assert E.load_library().gck_abi_version() == 2
+    assert E.load_library().gck_abi_version() == 3
 
 
 @pytest.fixture()
@@ -133,4 +134,11 @@ def test_state_errors(eng):
     assert ei.value.code == E.GCK_E_STATE
     with pytest.raises(E.GckError) as ei:
         eng.check_bulk(np.zeros(1, dtype=E.ITEM_DTYPE))
+    assert ei.value.code == E.GCK_E_STATE
+    # Watch updates need a committed snapshot
+    with pytest.raises(E.GckError) as ei:
+        eng.apply_updates_text(2, "CREATE user:a#x@user:b")
+    assert ei.value.code == E.GCK_E_STATE
+    with pytest.raises(E.GckError) as ei:
+        eng.apply_updates(2, np.zeros(1, dtype=E.UPDATE_DTYPE))
     assert ei.value.code == E.GCK_E_STATE
