@@ -192,6 +192,7 @@ def main():
     # sized to --cpu-seconds; the GPU result of every sampled check is compared with it.
     cpu = None
     agree = None
+    disagree = []
     if rank == 0 and world == 1 and not args.no_cpu and prog is not None:
         t0 = time.perf_counter()
         corc.check(prog, tab, host_items, threads=threads)
@@ -208,12 +209,25 @@ def main():
         host = [(b[0].cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1), b[1].cpu().numpy(), b[2].cpu().numpy())
                 for b in batches]
         n_s, n_ok, dt = 0, 0, 0.0
-        for hi, gp, ge in host:
+        for bi, (hi, gp, ge) in enumerate(host):
             t0 = time.perf_counter()
             cp, ce, _ = corc.check(prog, tab, hi, threads=threads)
             dt += time.perf_counter() - t0
             n_s += len(hi)
-            n_ok += int(((cp == gp) & (ce == ge)).sum())
+            ok = (cp == gp) & (ce == ge)
+            n_ok += int(ok.sum())
+            if not ok.all() and len(disagree) < 8:  # diagnostics: which batch, which items
+                bad = np.nonzero(~ok)[0]
+                # the same batch again, synchronously: does the engine agree the second time?
+                it = batches[bi][0]
+                pk, ek = torch.zeros_like(perm), torch.zeros_like(err)
+                eng.check_bulk_device(it.data_ptr(), args.batch, pk.data_ptr(), ek.data_ptr(), stream=stream)
+                torch.cuda.synchronize()
+                rp, re_ = pk.cpu().numpy(), ek.cpu().numpy()
+                disagree.append({"batch": bi, "n": int(len(bad)), "unwritten": int(((gp == 0) & (ge == 0)).sum()),
+                                 "rerun_mismatches": int(((rp != cp) | (re_ != ce)).sum()),
+                                 "first": [{"i": int(i), "gpu": [int(gp[i]), int(ge[i])],
+                                            "oracle": [int(cp[i]), int(ce[i])]} for i in bad[:3]]})
         agree = n_ok / n_s
         cpu = {"value": round(n_s / dt, 1), "unit": "checks/s", "cores": threads, "kind": "port",
                "sample": f"{len(host)} batches x {args.batch} checks (the timed batch + seeds 5000..), same "
@@ -233,6 +247,7 @@ def main():
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
             "roofline": roof, "cpu_baseline": cpu,
             "oracle_agreement": agree,
+            **({"disagreements": disagree} if disagree else {}),
             "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),
                            "COND": int((res == 3).sum()), "ERR": int((errs != 0).sum())},
             "engine": {"levels_per_batch": round(st["levels"] / n_batches, 1),

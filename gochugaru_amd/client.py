@@ -134,10 +134,10 @@ class Client:
         rels = [r.Relationship() for r in rs]
         try:
             requirement, revision = _requirement(cs)
-            items = self.engine.make_items(rels)
+            items, contexts = self.engine.make_request(rels)
             perm, err = retryRetriableErrors(
                 ctx or Background,
-                lambda: self.engine.check_bulk(items, requirement, revision))
+                lambda: self.engine.check_bulk(items, requirement, revision, contexts=contexts))
         except Exception as e:  # noqa: BLE001 — Go returns (nil, err)
             return None, e
         results: List[bool] = []

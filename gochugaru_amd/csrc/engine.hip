@@ -76,6 +76,8 @@ struct DeviceSnapshot {
   bool has_bidir = false;  // some forward node is NF_BIDIR
   uint32_t node_bits = 1, q_bits = 1;
   uint64_t bytes = 0;
+  uint8_t* cav_static = nullptr;  // per caveat instance (Engine::caveat_static)
+  uint32_t* cav_row = nullptr;    // per caveat instance (Engine::caveat_row)
 };
 
 struct Workspace {
@@ -114,6 +116,10 @@ struct Workspace {
   gck_item* def_items = nullptr;
   uint8_t* def_perm = nullptr;
   int32_t* def_err = nullptr;
+  // the current call's caveat outcome table (gck_api.cpp caveat_table), n_ctx columns
+  uint8_t* cav_dyn = nullptr;
+  size_t cav_dyn_cap = 0;
+  uint32_t n_ctx = 0;
   std::vector<void*> allocs;
 };
 
@@ -139,6 +145,14 @@ struct Ctx {
   uint32_t node_shift, q_shift;  // key = q << q_shift | node << node_shift | cond << 32 | obj
   uint32_t level, max_depth;
   int64_t now_us;
+  // caveats (cel.hpp; gck_api.cpp caveat_table): per instance its outcome under the stored
+  // context alone (0 false, 1 true, 2 partial) and, for partial ones, a row of the per-batch
+  // table of outcomes under each check context (column slot - 1)
+  const uint8_t* cav_static;
+  const uint32_t* cav_row;
+  const uint8_t* cav_dyn;
+  const gck_item* ck_items;  // the launch's items: check k's context slot
+  uint32_t n_ctx;
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -256,6 +270,23 @@ __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t n
   return x == 0 || x > now_us;
 }
 
+// Caveat instance `cav` on a path of the check whose item is `item`: 0 = the caveat is false
+// (the relationship does not count), 1 = true (a plain edge), 2 = unresolved (CONDITIONAL).
+__device__ __forceinline__ uint32_t cav_state(const Ctx& c, uint32_t cav, uint32_t item) {
+  const uint32_t s = gptr(c.cav_static)[cav];
+  if (s != 2u || c.n_ctx == 0) return s;
+  const uint32_t slot = gptr(c.ck_items)[item].context_slot;
+  if (slot == 0 || slot > c.n_ctx) return 2u;
+  return gptr(c.cav_dyn)[(size_t)gptr(c.cav_row)[cav] * c.n_ctx + (slot - 1)];
+}
+
+// An edge of an ext CSR under the check of `item`: 0 = absent (expired, or its caveat is
+// false), 1 = plain, 2 = conditional.
+__device__ __forceinline__ uint32_t ext_state(const Ctx& c, const DevCSR& r, uint32_t pos, uint32_t item) {
+  if (!visible(r, pos, c.now_us)) return 0u;
+  return cav_state(c, csr_cav(r, pos), item);
+}
+
 // Membership-index bucket scan: 1 = key present, 0 = absent (the bucket has an empty slot, so
 // no key homed here overflowed), 2 = bucket full without the key (continue with the next one).
 constexpr int kBucketKeys = 8;  // 8 x u64 = 64 B
@@ -299,9 +330,10 @@ __device__ __forceinline__ bool hash_member(const DevCSR& r, uint32_t obj, uint3
 }
 
 // checkDirect membership on one CSR: the subject itself (`direct`) and/or the wildcard
-// (`wild`). Returns 0 = absent, 1 = present, 2 = present through a caveated edge.
-__device__ __forceinline__ uint32_t member_test(const DevCSR& r, uint32_t obj, uint32_t sid, bool direct,
-                                                bool wild, int64_t now_us, uint32_t& rows,
+// (`wild`) for the check of `item`. Returns 0 = absent, 1 = present, 2 = present through a
+// caveat that stays unresolved.
+__device__ __forceinline__ uint32_t member_test(const Ctx& c, const DevCSR& r, uint32_t obj, uint32_t sid,
+                                                bool direct, bool wild, uint32_t item, uint32_t& rows,
                                                 uint32_t& probes) {
   if (obj >= r.n_rows) return 0;
   if (r.mhash) {  // plain direct CSR: hashed index, no row read
@@ -313,14 +345,14 @@ __device__ __forceinline__ uint32_t member_test(const DevCSR& r, uint32_t obj, u
   uint32_t best = 0;
   if (direct) {
     const uint32_t p = row_find(r, obj, sid, probes);
-    if (p != kNone && visible(r, p, now_us)) best = (r.is_ext && csr_cav(r, p) != 0) ? 2u : 1u;
+    if (p != kNone) best = r.is_ext ? ext_state(c, r, p, item) : 1u;
   }
   if (wild && best != 1) {
     const uint32_t b = csr_off(r, obj), en = csr_off(r, obj + 1);
     ++probes;
-    if (en > b && csr_nbr(r, en - 1) == kWildcard && visible(r, en - 1, now_us)) {
-      const uint32_t m = (r.is_ext && csr_cav(r, en - 1) != 0) ? 2u : 1u;
-      if (best == 0 || m == 1) best = m;
+    if (en > b && csr_nbr(r, en - 1) == kWildcard) {
+      const uint32_t m = r.is_ext ? ext_state(c, r, en - 1, item) : 1u;
+      if (m && (best == 0 || m == 1)) best = m;
     }
   }
   return best;
@@ -360,6 +392,7 @@ __device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_
 __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth,
                            uint32_t cond, uint32_t& rows) {
   const DevNode nd = c.nodes[node];
+  const uint32_t check = c.queries[q].check;
   uint32_t n_ops = 0;
   if (nd.kind == NK_ARROW_ALL) {
     bool missing = false;
@@ -374,7 +407,8 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
-          if (it.target == kNoNode) missing = true;
+          // a subject lacking the target, or one whose caveat is false, fails the all()
+          if (it.target == kNoNode || (r.is_ext && cav_state(c, csr_cav(r, p), check) == 0u)) missing = true;
           ++n_ops;
         }
       }
@@ -405,7 +439,6 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
   J.state = 0;
   J.pad = 0;
   c.joins[j] = J;
-  const uint32_t check = c.queries[q].check;
   for (uint32_t k = 0; k < n_ops; ++k) {
     DevQuery cq;
     cq.check = check;
@@ -429,7 +462,7 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
-          uint32_t cav = r.is_ext ? (csr_cav(r, p) != 0) : 0u;
+          const uint32_t cav = r.is_ext ? (uint32_t)(cav_state(c, csr_cav(r, p), check) == 2u) : 0u;
           push_entry(c, q0 + k, csr_nbr(r, p), it.target, depth + 1, cav);
           ++k;
         }
@@ -532,7 +565,7 @@ __global__ void __launch_bounds__(kBlock) k_expand(Ctx c, const Entry* __restric
               for (int pass = 0; pass < 2 && !done; ++pass) {
                 uint32_t ci = pass ? it.csr_ext : it.csr_plain;
                 if (ci == kNone) continue;
-                const uint32_t m = member_test(c.csrs[ci], e.obj, s.sid, direct, wild, c.now_us, rows, probes);
+                const uint32_t m = member_test(c, c.csrs[ci], e.obj, s.sid, direct, wild, q->check, rows, probes);
                 if (m) {
                   const uint32_t cond = e.cond | (m == 2);
                   set_found(c, e.q, cond);
@@ -606,8 +639,9 @@ __global__ void __launch_bounds__(kBlock) k_edges(Ctx c) {
     uint32_t cond = s.cond;
     if (r.is_ext) {
       ++ext_edges;
-      if (!visible(r, p, c.now_us)) continue;
-      cond |= (csr_cav(r, p) != 0);
+      const uint32_t st = ext_state(c, r, p, c.queries[s.q].check);
+      if (st == 0u) continue;
+      cond |= (st == 2u);
     }
     if (x == kWildcard) continue;
     push_entry(c, s.q, x, s.target, s.depth, cond);
@@ -1027,6 +1061,19 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     std::vector<uint32_t> counts(sc.types.size());
     for (size_t t = 0; t < counts.size(); ++t) counts[t] = e.interner[t].count;
     HIP_OK(hipMemcpy(ds->type_counts, counts.data(), counts.size() * 4, hipMemcpyHostToDevice));
+    // caveat instances: outcome under the stored context, row of the per-batch table
+    {
+      std::vector<uint8_t> st(e.caveat_static);
+      std::vector<uint32_t> row(e.caveat_row);
+      if (st.empty()) {
+        st.push_back(1);
+        row.push_back(kNone);
+      }
+      ds->cav_static = dalloc<uint8_t>(ds->allocs, st.size(), &ds->bytes);
+      ds->cav_row = dalloc<uint32_t>(ds->allocs, row.size(), &ds->bytes);
+      HIP_OK(hipMemcpy(ds->cav_static, st.data(), st.size(), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(ds->cav_row, row.data(), row.size() * 4, hipMemcpyHostToDevice));
+    }
     ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
     if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
     ds->q_bits = 31 - ds->node_bits;
@@ -1162,6 +1209,10 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.q_shift = 33 + ds.node_bits;
   c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
   c.now_us = now_us;
+  c.cav_static = ds.cav_static;
+  c.cav_row = ds.cav_row;
+  c.cav_dyn = w.cav_dyn;
+  c.n_ctx = w.cav_dyn ? w.n_ctx : 0u;
   (void)next_pow2_fits;
   return c;
 }
@@ -1169,6 +1220,7 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
 static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                       uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
   Ctx c = make_ctx(e, w, now_us);
+  c.ck_items = d_items;
   HIP_OK(hipEventRecord(w.ev0, st));
   HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
   HIP_OK(hipMemsetAsync(w.visited, 0xFF, w.visited_cap * sizeof(unsigned long long), st));
@@ -1260,6 +1312,7 @@ static void check_range_wide(Engine& e, Workspace& w, const gck_item* d_items, s
 static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                         uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
   Ctx c = make_ctx(e, w, now_us);
+  c.ck_items = d_items;
   const bool profile = (e.cfg.flags & GCK_FLAG_PROFILE) != 0;
   BundleArgs a{};
   a.items = d_items;
@@ -1429,12 +1482,32 @@ static int64_t wall_now_us() {
   return duration_cast<microseconds>(system_clock::now().time_since_epoch()).count();
 }
 
+// Stages the call's caveat outcome table (n_ctx columns; empty = no check contexts).
+static void stage_caveats(Workspace& w, const std::vector<uint8_t>& table, uint32_t n_ctx, hipStream_t st) {
+  w.n_ctx = table.empty() ? 0u : n_ctx;
+  if (table.empty()) return;
+  if (w.cav_dyn_cap < table.size()) {
+    if (w.cav_dyn) {
+      HIP_OK(hipStreamSynchronize(st));
+      w.allocs.erase(std::remove(w.allocs.begin(), w.allocs.end(), (void*)w.cav_dyn), w.allocs.end());
+      HIP_OK(hipFree(w.cav_dyn));
+      w.cav_dyn = nullptr;
+    }
+    w.cav_dyn_cap = std::max(table.size(), w.cav_dyn_cap * 2);
+    w.cav_dyn = dalloc<uint8_t>(w.allocs, w.cav_dyn_cap);
+  }
+  HIP_OK(hipMemcpyAsync(w.cav_dyn, table.data(), table.size(), hipMemcpyHostToDevice, st));
+}
+
 void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
-                  int32_t* d_err, void* stream) {
+                  int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
   HIP_OK(hipSetDevice(e.device));
   std::lock_guard<std::mutex> lk(e.ws_mu);
   Workspace& w = *ensure_workspace(e);
-  hipStream_t st = stream ? (hipStream_t)stream : w.stream;
+  // the caller's stream; NULL is the legacy default stream (never the engine's own non-blocking
+  // stream, which would not be ordered after the caller's writes of the items and outputs)
+  hipStream_t st = (hipStream_t)stream;
+  stage_caveats(w, cav_table, n_ctx, st);
   if (now_us == 0) now_us = wall_now_us();
   float ms = 0.f;
   check_range(e, w, d_items, n, now_us, d_perm, d_err, st, &ms);
@@ -1442,10 +1515,11 @@ void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, 
 }
 
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                       int32_t* err) {
+                       int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
   HIP_OK(hipSetDevice(e.device));
   std::lock_guard<std::mutex> lk(e.ws_mu);
   Workspace& w = *ensure_workspace(e);
+  stage_caveats(w, cav_table, n_ctx, w.stream);
   if (now_us == 0) now_us = wall_now_us();
   float ms = 0.f;
   size_t pos = 0;

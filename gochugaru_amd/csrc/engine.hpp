@@ -10,6 +10,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "cel.hpp"
 #include "gck.h"
 #include "gck_internal.hpp"
 
@@ -54,6 +55,7 @@ struct CaveatDef {
   std::string name;
   std::vector<std::pair<std::string, std::string>> params;
   std::string body;
+  std::shared_ptr<const cel::Node> expr;  // compiled body (cel.hpp)
 };
 
 struct Schema {
@@ -138,7 +140,14 @@ struct Engine {
   std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
   std::unique_ptr<Schema> schema;
   std::vector<TypeInterner> interner;
-  std::vector<std::pair<std::string, std::string>> caveat_instances;  // [0] = none
+  // caveat instances: a caveat name + stored context, deduplicated; [0] = none (gck_api.cpp)
+  std::vector<std::pair<std::string, std::string>> caveat_instances;
+  std::unordered_map<std::string, uint32_t> caveat_ids;       // name '\0' json -> instance
+  std::vector<std::shared_ptr<const cel::Node>> caveat_expr;  // per instance (null for [0])
+  std::vector<cel::Object> caveat_ctx;                        // per instance: stored context
+  std::vector<uint8_t> caveat_static;   // per instance: cel::Outcome under the stored context alone
+  std::vector<uint32_t> caveat_row;     // per instance: row of the per-call table (PARTIAL only)
+  std::vector<uint32_t> caveat_partial; // row -> instance
   // staging
   bool staging = false;
   uint64_t staged_revision = 0;
@@ -167,10 +176,13 @@ std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>&
 int device_init(Engine& e);
 void device_upload(Engine& e, std::vector<HostCSR>& csrs);
 void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
+// cav_table: the call's caveat outcome table (row = partial instance, n_ctx columns = check
+// contexts 1..n_ctx; empty when the call has no check contexts)
 void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
-                  uint8_t* d_perm, int32_t* d_err, void* stream);
+                  uint8_t* d_perm, int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table,
+                  uint32_t n_ctx);
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
-                       uint8_t* perm, int32_t* err);
+                       uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
 uint64_t device_bytes(const Engine& e);
 void device_free(Engine& e);
 

@@ -9,12 +9,76 @@ namespace gck {
 
 thread_local std::string g_last_error;
 
+#define REQUIRE(cond, code, msg) \
+  do {                           \
+    if (!(cond)) throw Error(code, msg); \
+  } while (0)
+
 Engine::~Engine() { device_free(*this); }
 
+static void reset_caveats(Engine& e) {
+  e.caveat_instances.assign(1, {"", ""});
+  e.caveat_ids.clear();
+  e.caveat_expr.assign(1, nullptr);
+  e.caveat_ctx.assign(1, cel::Object{});
+  e.caveat_static.assign(1, (uint8_t)cel::TRUE);  // instance 0: no caveat
+  e.caveat_row.assign(1, kNone);
+  e.caveat_partial.clear();
+}
+
+// A caveat name + stored context (rel.Relationship.CaveatName/CaveatContext,
+// rel/relationship.go:93-120). Identical pairs share one instance. The stored context is parsed
+// and the expression evaluated over it alone once, here: a caveat it decides is a plain or an
+// absent edge for every check; one left PARTIAL gets a row of the per-call outcome table.
 uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json) {
-  if (!e.schema->caveats.count(name)) throw Error(GCK_E_INVALID_ARGUMENT, "unknown caveat '" + name + "'");
+  auto cd = e.schema->caveats.find(name);
+  if (cd == e.schema->caveats.end()) throw Error(GCK_E_INVALID_ARGUMENT, "unknown caveat '" + name + "'");
+  std::string key = name;
+  key += '\0';
+  key += json;
+  auto hit = e.caveat_ids.find(key);
+  if (hit != e.caveat_ids.end()) return hit->second;
+  REQUIRE(e.caveat_instances.size() < 0xFFFFFFF0u, GCK_E_CAPACITY, "too many caveat instances");
+  cel::Object ctx = cel::parse_context(json);
+  const cel::Outcome o = cel::evaluate(*cd->second.expr, &ctx, nullptr);
+  const uint32_t id = (uint32_t)e.caveat_instances.size();
   e.caveat_instances.emplace_back(name, json);
-  return (uint32_t)(e.caveat_instances.size() - 1);
+  e.caveat_expr.push_back(cd->second.expr);
+  e.caveat_ctx.push_back(std::move(ctx));
+  e.caveat_static.push_back((uint8_t)o);
+  e.caveat_row.push_back(o == cel::PARTIAL ? (uint32_t)e.caveat_partial.size() : kNone);
+  if (o == cel::PARTIAL) e.caveat_partial.push_back(id);
+  e.caveat_ids.emplace(std::move(key), id);
+  return id;
+}
+
+// The outcome table of one check call: row r = partial instance caveat_partial[r], column k =
+// check context k + 1 (CheckBulkPermissionsRequestItem.Context, client/client.go:257), each
+// merged under the instance's stored context. Identical context texts share a column's
+// evaluation.
+static std::vector<uint8_t> caveat_table(Engine& e, const char* const* ctxs, const size_t* lens, size_t n_ctx) {
+  std::vector<uint8_t> t;
+  const size_t rows = e.caveat_partial.size();
+  if (n_ctx == 0 || rows == 0) return t;
+  REQUIRE(rows * n_ctx <= (1ull << 30), GCK_E_CAPACITY,
+          "caveat outcome table too large (partial caveat instances x check contexts)");
+  t.resize(rows * n_ctx);
+  std::unordered_map<std::string, size_t> seen;
+  for (size_t k = 0; k < n_ctx; ++k) {
+    std::string js(ctxs[k] ? ctxs[k] : "", ctxs[k] ? lens[k] : 0);
+    auto it = seen.find(js);
+    if (it != seen.end()) {
+      for (size_t r = 0; r < rows; ++r) t[r * n_ctx + k] = t[r * n_ctx + it->second];
+      continue;
+    }
+    const cel::Object ctx = cel::parse_context(js);
+    for (size_t r = 0; r < rows; ++r) {
+      const uint32_t id = e.caveat_partial[r];
+      t[r * n_ctx + k] = (uint8_t)cel::evaluate(*e.caveat_expr[id], &e.caveat_ctx[id], &ctx);
+    }
+    seen.emplace(std::move(js), k);
+  }
+  return t;
 }
 
 void stage_tuple(Engine& e, const gck_tuple& t);
@@ -44,11 +108,6 @@ static int guard(F&& f) {
     return GCK_E_INVALID_ARGUMENT;
   }
 }
-
-#define REQUIRE(cond, code, msg) \
-  do {                           \
-    if (!(cond)) throw Error(code, msg); \
-  } while (0)
 
 static Engine& need(gck_engine* e) {
   REQUIRE(e, GCK_E_INVALID_ARGUMENT, "null engine");
@@ -80,7 +139,7 @@ int gck_create(const gck_config* cfg, gck_engine** out) {
       delete e;
       throw Error(GCK_E_INVALID_ARGUMENT, "bad device ordinal");
     }
-    e->impl.caveat_instances.emplace_back("", "");
+    reset_caveats(e->impl);
     *out = e;
   });
 }
@@ -95,7 +154,7 @@ int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
     std::unique_lock<std::shared_mutex> lk(e.mu);
     e.schema = std::move(sc);
     e.interner.assign(e.schema->types.size(), TypeInterner());
-    e.caveat_instances.assign(1, {"", ""});
+    reset_caveats(e);
     e.staged.clear();
     e.prebuilt.clear();
     e.staging = false;
@@ -219,6 +278,20 @@ int gck_add_caveat_instance(gck_engine* ge, const char* name, size_t name_len, c
     REQUIRE(name && out_id, GCK_E_INVALID_ARGUMENT, "null argument");
     std::unique_lock<std::shared_mutex> lk(e.mu);
     *out_id = add_caveat_instance(e, std::string(name, name_len), std::string(json ? json : "", json_len));
+  });
+}
+
+int gck_evaluate_caveat(gck_engine* ge, const char* name, size_t name_len, const char* stored_json,
+                        size_t stored_len, const char* context_json, size_t context_len, uint8_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    Schema& sc = need_schema(e);
+    REQUIRE(name && out, GCK_E_INVALID_ARGUMENT, "null argument");
+    auto cd = sc.caveats.find(std::string(name, name_len));
+    REQUIRE(cd != sc.caveats.end(), GCK_E_NOT_FOUND, "unknown caveat '" + std::string(name, name_len) + "'");
+    const cel::Object st = cel::parse_context(std::string(stored_json ? stored_json : "", stored_json ? stored_len : 0));
+    const cel::Object cx = cel::parse_context(std::string(context_json ? context_json : "", context_json ? context_len : 0));
+    *out = (uint8_t)cel::evaluate(*cd->second.expr, &st, &cx);
   });
 }
 
@@ -398,29 +471,51 @@ static void check_consistency(Engine& e, const gck_consistency* cs) {
   }
 }
 
-int gck_check_bulk(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
-                   int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
+int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                       const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                       int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
   return guard([&] {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
+    REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
     check_consistency(e, cs);
     if (n == 0) return;  // empty request -> empty response (client/client_test.go:203-207)
-    device_check_host(e, items, n, now_us, out_perm, out_err);
+    for (size_t i = 0; i < n; ++i)
+      REQUIRE(items[i].context_slot <= n_contexts, GCK_E_INVALID_ARGUMENT,
+              "item " + std::to_string(i) + ": context_slot " + std::to_string(items[i].context_slot) +
+                  " beyond the " + std::to_string(n_contexts) + " contexts given");
+    const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
+    device_check_host(e, items, n, now_us, out_perm, out_err, table, (uint32_t)n_contexts);
   });
 }
 
-int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us,
-                          uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
+int gck_check_bulk(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                   int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
+  return gck_check_bulk_ctx(ge, cs, items, n, nullptr, nullptr, 0, now_us, out_perm, out_err);
+}
+
+int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n, const char* const* contexts,
+                              const size_t* context_lens, size_t n_contexts, int64_t now_us,
+                              uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
   return guard([&] {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
+    REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
     if (n == 0) return;
-    device_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream);
+    const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
+    device_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream, table, (uint32_t)n_contexts);
   });
+}
+
+int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us,
+                          uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
+  return gck_check_bulk_device_ctx(ge, d_items, n, nullptr, nullptr, 0, now_us, d_out_perm, d_out_err, stream);
 }
 
 int gck_last_stats(gck_engine* ge, gck_stats* out) {

@@ -8,6 +8,7 @@ HIP device is missing, the calls fail loudly.
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 from typing import Iterable, List, Optional, Sequence, Tuple
 
@@ -42,6 +43,7 @@ TYPE_INVALID = 0xFFFF
 REL_INVALID = 0xFFFE  # an id no schema relation has (never equal to ELLIPSIS)
 
 CONSISTENCY_MIN_LATENCY, CONSISTENCY_FULL, CONSISTENCY_AT_LEAST, CONSISTENCY_SNAPSHOT = 0, 1, 2, 3
+CAVEAT_FALSE, CAVEAT_TRUE, CAVEAT_PARTIAL = 0, 1, 2
 INTERN_CREATE = 1
 MEM_DEVICE = 1
 FLAG_PROFILE = 1
@@ -134,6 +136,8 @@ _SIGS = {
                                   C.POINTER(C.c_size_t)]),
     "gck_add_caveat_instance": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
                                           C.POINTER(C.c_uint32)]),
+    "gck_evaluate_caveat": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p,
+                                      C.c_size_t, C.POINTER(C.c_uint8)]),
     "gck_begin_snapshot": (C.c_int, [_P, C.c_uint64]),
     "gck_add_tuples": (C.c_int, [_P, _P, C.c_size_t]),
     "gck_add_tuples_text": (C.c_int, [_P, C.c_char_p, C.c_size_t]),
@@ -147,6 +151,10 @@ _SIGS = {
     "gck_apply_updates_text": (C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "gck_check_bulk": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.c_int64, _P, _P]),
     "gck_check_bulk_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
+    "gck_check_bulk_ctx": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.POINTER(C.c_char_p),
+                                     C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P]),
+    "gck_check_bulk_device_ctx": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                            C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
     "gck_reset_stats": (C.c_int, [_P]),
 }
@@ -303,6 +311,15 @@ class Engine:
         _check(self._lib.gck_add_caveat_instance(self._h, nb, len(nb), jb, len(jb), C.byref(out)))
         return out.value
 
+    def evaluate_caveat(self, name: str, stored=None, context=None) -> int:
+        """The host CEL evaluator: CAVEAT_FALSE / CAVEAT_TRUE / CAVEAT_PARTIAL."""
+        out = C.c_uint8()
+        nb = name.encode()
+        sb = _context_json(stored).encode()
+        cb = _context_json(context).encode()
+        _check(self._lib.gck_evaluate_caveat(self._h, nb, len(nb), sb, len(sb), cb, len(cb), C.byref(out)))
+        return out.value
+
     # ---- snapshot ------------------------------------------------------------------------
     def begin_snapshot(self, revision: int):
         _check(self._lib.gck_begin_snapshot(self._h, revision))
@@ -368,21 +385,28 @@ class Engine:
 
     # ---- checks --------------------------------------------------------------------------
     def check_bulk(self, items: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY,
-                   revision: int = 0, now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+                   revision: int = 0, now_us: int = 0,
+                   contexts: Optional[Sequence] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """`contexts`: check-time caveat contexts (dicts or JSON text); an item's context_slot
+        k selects contexts[k-1] (make_request builds both)."""
         items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
         n = len(items)
         perm = np.zeros(n, dtype=np.uint8)
         err = np.zeros(n, dtype=np.int32)
         cs = _Consistency(requirement, 0, revision)
-        _check(self._lib.gck_check_bulk(self._h, C.byref(cs), items.ctypes.data if n else None, n,
-                                        now_us, perm.ctypes.data if n else None,
-                                        err.ctypes.data if n else None))
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        _check(self._lib.gck_check_bulk_ctx(self._h, C.byref(cs), items.ctypes.data if n else None, n,
+                                            ctx_arr, ctx_lens, n_ctx, now_us,
+                                            perm.ctypes.data if n else None,
+                                            err.ctypes.data if n else None))
         return perm, err
 
     def check_bulk_device(self, d_items: int, n: int, d_perm: int, d_err: int,
-                          stream: Optional[int] = None, now_us: int = 0):
-        _check(self._lib.gck_check_bulk_device(self._h, d_items, n, now_us, d_perm, d_err,
-                                               stream))
+                          stream: Optional[int] = None, now_us: int = 0,
+                          contexts: Optional[Sequence] = None):
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        _check(self._lib.gck_check_bulk_device_ctx(self._h, d_items, n, ctx_arr, ctx_lens, n_ctx, now_us,
+                                                   d_perm, d_err, stream))
 
     def stats(self) -> Stats:
         s = _Stats()
@@ -393,6 +417,26 @@ class Engine:
         _check(self._lib.gck_reset_stats(self._h))
 
     # ---- string-level convenience --------------------------------------------------------
+    def make_request(self, rels: Iterable) -> Tuple[np.ndarray, List[str]]:
+        """Items plus their check-time caveat contexts, as Client.Check builds them
+        (client/client.go:244-258: Context = MustV1ProtoCaveat().GetContext(), i.e. the
+        relationship's caveat context when it names a caveat). Identical contexts share a slot."""
+        rels = list(rels)
+        items = self.make_items(rels)
+        contexts: List[str] = []
+        slots = {}
+        for i, r in enumerate(rels):
+            ctx = r.MustV1ProtoCaveatContext() if hasattr(r, "MustV1ProtoCaveatContext") else None
+            if ctx is None:
+                continue
+            js = _context_json(ctx)
+            k = slots.get(js)
+            if k is None:
+                contexts.append(js)
+                k = slots[js] = len(contexts)
+            items[i]["context_slot"] = k
+        return items, contexts
+
     def make_items(self, rels: Iterable) -> np.ndarray:
         """rel.Relationship-like items -> interned gck_item array (unknown names map to
         invalid ids so the device reports the per-item error; unknown ids map to ABSENT)."""
@@ -422,3 +466,20 @@ class Engine:
             if items[i]["subject_type"] == TYPE_INVALID:
                 items[i]["subject_id"] = ID_WILDCARD if r.SubjectID == "*" else ID_ABSENT
         return items
+
+
+def _context_json(ctx) -> str:
+    if ctx is None:
+        return ""
+    if isinstance(ctx, (str, bytes)):
+        return ctx.decode() if isinstance(ctx, bytes) else ctx
+    return json.dumps(ctx, sort_keys=True, separators=(",", ":"))
+
+
+def _context_arrays(contexts):
+    if not contexts:
+        return None, None, 0
+    enc = [_context_json(c).encode() for c in contexts]
+    arr = (C.c_char_p * len(enc))(*enc)
+    lens = (C.c_size_t * len(enc))(*[len(b) for b in enc])
+    return arr, lens, len(enc)

@@ -21,6 +21,9 @@
  *   gck_apply_updates / gck_apply_updates_text
  *       consume the rel.Update stream of Client.UpdatesSinceRevision (client/client.go:370-413,
  *       rel.UpdateFromV1Proto rel/relationship.go:296-301) and keep the snapshot current.
+ *   gck_check_bulk_ctx / gck_check_bulk_device_ctx
+ *       additionally take the check-time caveat contexts (CheckBulkPermissionsRequestItem.Context,
+ *       client/client.go:257, from rel.Relationship.MustV1ProtoCaveat rel/relationship.go:174-188).
  *   gck_revision / gck_check_bulk's consistency argument
  *       honour consistency.Strategy (consistency/consistency.go:15-77) as sent in
  *       CheckBulkPermissionsRequest.Consistency (client/client.go:263).
@@ -40,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 3
+#define GCK_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -121,7 +124,8 @@ typedef struct gck_item {
   uint16_t subject_type;
   uint16_t subject_relation;   /* GCK_ELLIPSIS for a concrete object */
   uint32_t subject_id;
-  uint32_t context_slot;       /* 0 = no check-time caveat context */
+  uint32_t context_slot;       /* 0 = no check-time caveat context; k = contexts[k-1] of the
+                                  gck_check_bulk*_ctx call */
 } gck_item;                    /* 20 bytes */
 
 /* One relationship, interned: rel.Relationship (rel/relationship.go:28-38). */
@@ -200,8 +204,17 @@ int gck_object_name(gck_engine* e, uint16_t type, uint32_t id, char* buf, size_t
                     size_t* out_len);
 
 /* ---- caveats (rel.Relationship.CaveatName/CaveatContext) ------------------------------ */
+/* A caveat name with its stored context (a JSON object; "" = none). Identical (name, context)
+ * pairs return the same id. Errors: GCK_E_INVALID_ARGUMENT for an unknown caveat, malformed
+ * JSON, or a stored context on which the expression fails to evaluate. */
 int gck_add_caveat_instance(gck_engine* e, const char* name, size_t name_len,
                             const char* context_json, size_t json_len, uint32_t* out_id);
+
+/* The host CEL evaluator on its own: caveat `name` over the stored context merged with the
+ * check context (stored values take precedence). *out = 0 false, 1 true, 2 partial (a
+ * parameter is missing: CONDITIONAL). GCK_E_NOT_FOUND for an unknown caveat. */
+int gck_evaluate_caveat(gck_engine* e, const char* name, size_t name_len, const char* stored_json,
+                        size_t stored_len, const char* context_json, size_t context_len, uint8_t* out);
 
 /* ---- snapshot ingest (Client.ExportRelationships, client/client.go:472-499) ----------- */
 int gck_begin_snapshot(gck_engine* e, uint64_t revision);
@@ -234,13 +247,30 @@ int gck_apply_updates_text(gck_engine* e, uint64_t revision, const char* text, s
 /* ---- checks (CheckBulkPermissions, client/client.go:261-283) -------------------------- */
 /* Host buffers: items[n] in, out_perm[n] (GCK_PERM_*), out_err[n] (GCK_ITEM_*) out.
  * `now_us` = the evaluation time for expiring relationships (unix microseconds; 0 = wall
- * clock). Results are in request order. */
+ * clock). Results are in request order. Caveats are evaluated with the stored context only;
+ * one that depends on a missing parameter makes its path CONDITIONAL. */
 int gck_check_bulk(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
                    int64_t now_us, uint8_t* out_perm, int32_t* out_err);
-/* Device-resident buffers on the engine's device; `stream` is a hipStream_t (NULL = the
- * engine's own stream). Returns after the results are written (stream synchronised). */
+/* Same, with check-time caveat contexts: contexts[k] (JSON object text, context_lens[k] bytes)
+ * is the context of every item whose context_slot is k + 1. A caveat is evaluated over its
+ * stored context merged with the item's context (stored values take precedence): true = the
+ * relationship counts, false = it does not, missing parameter = CONDITIONAL.
+ * Errors: GCK_E_INVALID_ARGUMENT (a context_slot > n_contexts, malformed JSON, a CEL evaluation
+ * error), GCK_E_CAPACITY (partial caveat instances x contexts above 2^30). */
+int gck_check_bulk_ctx(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
+                       const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                       int64_t now_us, uint8_t* out_perm, int32_t* out_err);
+/* Device-resident buffers on the engine's device. `stream` is the hipStream_t the caller
+ * produced the items on and will read the results on; NULL is HIP's default (null) stream, as
+ * for any HIP launch, so work the caller queued there (e.g. PyTorch's default stream) is
+ * ordered before the check. Returns after the results are written (stream synchronised). */
 int gck_check_bulk_device(gck_engine* e, const gck_item* d_items, size_t n, int64_t now_us,
                           uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
+/* Device buffers with host-side check contexts (as gck_check_bulk_ctx; a device item's
+ * context_slot beyond n_contexts counts as no context). */
+int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
+                              const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                              int64_t now_us, uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
 

@@ -19,7 +19,7 @@ def main():
         sc, t, ch = gen.FAMILIES[fam](1)
         cases.append((fam, sc, t, ch))
     for name, schema, tuples, checks in cases:
-        ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6, evaluate_caveats=False)
+        ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
         want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
         for path, kw in sorted(PATHS.items()):
             e = make_engine(schema, tuples, **kw)

@@ -292,6 +292,14 @@ def gdocs_deep(seed, n_users=80, n_groups=40, n_folders=40, n_docs=60):
     return GDOCS, t, checks
 
 
+def check_contexts(seed, n):
+    """Check-time caveat contexts for n checks (CheckBulkPermissionsRequestItem.Context):
+    none, a satisfying one or a failing one for only_on_tuesday, and an unrelated key."""
+    rng = random.Random(seed * 7919 + 17)
+    opts = [None, None, {"day_of_the_week": "tuesday"}, {"day_of_the_week": "monday"}, {"other": 1}]
+    return [rng.choice(opts) for _ in range(n)]
+
+
 FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested,
             "gdocs_deep": gdocs_deep}
 NOW_US = 1759449600 * 1_000_000  # 2025-10-03T00:00:00Z

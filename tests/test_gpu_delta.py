@@ -97,7 +97,7 @@ def engine_results(e, checks):
 
 
 def oracle_results(schema, store, checks):
-    ck = oracle_for(schema, list(store.values()), now=gen.NOW_US / 1e6, evaluate_caveats=False)
+    ck = oracle_for(schema, list(store.values()), now=gen.NOW_US / 1e6)
     return [ck.check(to_oracle_item(parse_check(c))) for c in checks]
 
 

@@ -1,6 +1,8 @@
 """GPU parity: the HIP engine (through the C ABI) against the reference's known answers, the
 hand-derived SpiceDB-semantics fixtures and the Python oracle on seeded random graphs.
 Bar: bit-exact tri-state (HAS / NO / CONDITIONAL) and per-item error codes."""
+import json
+
 import numpy as np
 import pytest
 
@@ -27,9 +29,19 @@ def make_engine(schema, tuples, revision=1, **kw):
     return e
 
 
-def device_results(e, checks, now_us=NOW_US):
+def device_results(e, checks, now_us=NOW_US, contexts=None):
+    """Check strings through gck_check_bulk_ctx; contexts[i] is check i's caveat context."""
     items = e.make_items([parse_check(s) for s in checks])
-    perm, err = e.check_bulk(items, now_us=now_us)
+    texts, slots = [], {}
+    for i, ctx in enumerate(contexts or []):
+        if ctx is None:
+            continue
+        js = json.dumps(ctx, sort_keys=True)
+        if js not in slots:
+            texts.append(js)
+            slots[js] = len(texts)
+        items[i]["context_slot"] = slots[js]
+    perm, err = e.check_bulk(items, now_us=now_us, contexts=texts)
     return [(int(p), int(x)) for p, x in zip(perm, err)]
 
 
@@ -136,12 +148,18 @@ def test_semantics_depth():
         e.close()
 
 
-def test_semantics_caveats_device_contract():
+def test_semantics_caveats():
+    """Hand-derived caveat cases with their check contexts: the host evaluates each caveat
+    instance under each context (cel.cpp) and the device walk uses the outcomes."""
     s = _suite("caveats-and-expiration")
     e = make_engine(s["schema"], s["tuples"])
-    got = device_results(e, [c[0] for c in s["caveat_checks"]])
-    for c, g in zip(s["caveat_checks"], got):
-        assert g == expected_code(c[2]), c
+    rows = s["caveat_checks"]
+    got = device_results(e, [c[0] for c in rows], contexts=[c[1] for c in rows])
+    for c, g in zip(rows, got):
+        assert g == expected_code(c[3]), c
+    # one at a time (each call its own context table) gives the same answers
+    for c in rows:
+        assert device_results(e, [c[0]], contexts=[c[1]]) == [expected_code(c[3])], c
     e.close()
 
 
@@ -180,10 +198,11 @@ PATHS = {
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_random_parity(family, seed, path):
     schema, tuples, checks = gen.FAMILIES[family](seed)
-    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6, evaluate_caveats=False)
-    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+    contexts = gen.check_contexts(seed, len(checks))
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c), x)) for c, x in zip(checks, contexts)]
     e = make_engine(schema, tuples, **PATHS[path])
-    got = device_results(e, checks, now_us=gen.NOW_US)
+    got = device_results(e, checks, now_us=gen.NOW_US, contexts=contexts)
     bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
     assert not bad, bad[:10]
     if path == "bundle-deferred" and family != "caveated":  # caveated graphs are too small to overflow
@@ -204,8 +223,9 @@ def test_semantics_all_paths(path):
         if not rows:
             continue
         e = make_engine(s["schema"], s["tuples"], **PATHS[path])
-        got = device_results(e, [c[0] for c in rows])
-        col = 1 if "checks" in s else 2
+        ctxs = None if "checks" in s else [c[1] for c in rows]
+        got = device_results(e, [c[0] for c in rows], contexts=ctxs)
+        col = 1 if "checks" in s else 3
         assert got == [expected_code(c[col]) for c in rows], s["name"]
         e.close()
 
@@ -255,4 +275,73 @@ def test_device_buffers_api():
                         stream=torch.cuda.current_stream().cuda_stream, now_us=gen.NOW_US)
     assert np.array_equal(d_perm.cpu().numpy(), want_p)
     assert np.array_equal(d_err.cpu().numpy(), want_e)
+    e.close()
+
+
+def test_device_buffers_api_with_contexts():
+    """gck_check_bulk_device_ctx: device-resident items, host-side check contexts."""
+    import torch
+    schema, tuples, checks = gen.caveated(2)
+    contexts = gen.check_contexts(2, len(checks))
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c), x)) for c, x in zip(checks, contexts)]
+    e = make_engine(schema, tuples)
+    items = e.make_items([parse_check(c) for c in checks])
+    texts = []
+    for i, x in enumerate(contexts):
+        if x is not None:
+            texts.append(json.dumps(x))
+            items[i]["context_slot"] = len(texts)
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    d_perm = torch.zeros(len(items), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(len(items), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    e.check_bulk_device(d_items.data_ptr(), len(items), d_perm.data_ptr(), d_err.data_ptr(),
+                        stream=torch.cuda.current_stream().cuda_stream, now_us=gen.NOW_US, contexts=texts)
+    got = [(int(p), int(x)) for p, x in zip(d_perm.cpu().numpy(), d_err.cpu().numpy())]
+    assert got == want
+    e.close()
+
+
+def test_client_check_sends_caveat_context():
+    """Client.Check passes rel.Relationship's caveat context as the check context
+    (client/client.go:257); CONDITIONAL maps to false (client/client.go:274-277)."""
+    s = _suite("caveats-and-expiration")
+    e = make_engine(s["schema"], s["tuples"])
+    c = Client(e)
+    r = rel.MustFromTriple("doc:a", "viewer", "user:u1")
+    ok, err = c.CheckOne(None, consistency.MinLatency(), r)
+    assert err is None and ok is False  # CONDITIONAL
+    ok, err = c.CheckOne(None, consistency.MinLatency(), r.WithCaveat("only_on_tuesday", {"day_of_the_week": "tuesday"}))
+    assert err is None and ok is True
+    res, err = c.Check(None, consistency.MinLatency(),
+                       r.WithCaveat("only_on_tuesday", {"day_of_the_week": "monday"}),
+                       r.WithCaveat("only_on_tuesday", {"day_of_the_week": "tuesday"}),
+                       rel.MustFromTriple("doc:a", "view", "user:u2"))
+    assert err is None and res == [False, True, True]
+    e.close()
+
+
+def test_device_api_is_ordered_after_callers_stream():
+    """Regression: with stream=NULL (PyTorch's default stream) the check must run after work
+    the caller queued there — here a long kernel followed by writes of the items and outputs."""
+    import torch
+    schema, tuples, checks = gen.nested(4)
+    e = make_engine(schema, tuples)
+    items = e.make_items([parse_check(c) for c in checks])
+    want_p, want_e = e.check_bulk(items, now_us=gen.NOW_US)
+    host_items = torch.from_numpy(items.view(np.uint8).copy())
+    for _ in range(4):
+        d_items = torch.zeros(host_items.numel(), dtype=torch.uint8, device="cuda")
+        d_perm = torch.zeros(len(items), dtype=torch.uint8, device="cuda")
+        d_err = torch.zeros(len(items), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        torch.cuda._sleep(50_000_000)  # keep the default stream busy
+        d_items.copy_(host_items.cuda(non_blocking=True))
+        d_perm.fill_(7)
+        d_err.fill_(-1)
+        e.check_bulk_device(d_items.data_ptr(), len(items), d_perm.data_ptr(), d_err.data_ptr(),
+                            stream=torch.cuda.current_stream().cuda_stream, now_us=gen.NOW_US)
+        assert np.array_equal(d_perm.cpu().numpy(), want_p)
+        assert np.array_equal(d_err.cpu().numpy(), want_e)
     e.close()
