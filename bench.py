@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--no-giant", action="store_true", help="deferred checks go to the grid-wide path")
     ap.add_argument("--no-bidir", action="store_true", help="forward-only search (no bidirectional checks)")
     ap.add_argument("--bidir-both", type=int, default=0, help="expand both sides while <= this many entries")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="config 4 partitioned mode: each rank holds the rows it owns; the ranks check one "
+                         "global batch (batch x ranks) with a per-level all-to-all (gochugaru_amd/partition.py)")
+    ap.add_argument("--part-backend", default="nccl", help="exchange backend in --partitioned mode (nccl = RCCL)")
+    ap.add_argument("--share-gpu", action="store_true", help="every rank on cuda:0 (a one-GPU rehearsal with gloo)")
     return ap.parse_args()
 
 
@@ -66,10 +71,12 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")  # only timing barriers/reductions; no data-path collective
+        # replicated mode: gloo for the timing barriers / reductions only (no data-path collective);
+        # partitioned mode: the per-level exchange (RCCL over xGMI by default)
+        dist.init_process_group(args.part_backend if args.partitioned else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -82,11 +89,14 @@ def main():
     t_gen = time.time() - t0
 
     t0 = time.time()
-    eng = Engine(device=local, profile=not args.no_profile, wide_only=args.wide_only,
+    eng = Engine(device=local, profile=not args.no_profile,
+                 max_batch=args.batch * world if args.partitioned else args.batch, wide_only=args.wide_only,
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
                  bundle_budget=args.bundle_budget, giant_slots=args.giant_slots,
                  giant_stage=not args.no_giant, bidir=not args.no_bidir, bidir_both=args.bidir_both)
+    if args.partitioned:
+        eng.set_partition(rank, world)
     eng.load_schema(synth.SCHEMA)
     assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
     assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW
@@ -106,13 +116,24 @@ def main():
     n_tuples = eng.tuple_count
     dev_bytes = eng.device_bytes
 
-    items = synth.checks(G, args.batch, seed=1000 + rank)
-    perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
-    err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    if args.partitioned:
+        # one global batch: every rank's 64K checks, the same items on every rank
+        from gochugaru_amd.partition import PartitionedChecker
+        pc = PartitionedChecker(eng)
+        items = torch.cat([synth.checks(G, args.batch, seed=1000 + r) for r in range(world)])
+        n_global = args.batch * world
+        out = {}
 
-    def step():
-        eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream)
+        def step():
+            out["perm"], out["err"] = pc.check(items, n_global)
+    else:
+        items = synth.checks(G, args.batch, seed=1000 + rank)
+        perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
+        err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+
+        def step():
+            eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -137,6 +158,10 @@ def main():
     total_checks = world * args.batch * args.steps
     value = total_checks / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    if args.partitioned:  # this rank's slice of the global batch, for the checker below
+        perm = out["perm"][rank * args.batch:(rank + 1) * args.batch].contiguous()
+        err = out["err"][rank * args.batch:(rank + 1) * args.batch].contiguous()
+        items = items[rank * args.batch:(rank + 1) * args.batch].contiguous()
     res = perm.cpu().numpy()
     errs = err.cpu().numpy()
 
@@ -167,7 +192,7 @@ def main():
     # the mean of HIP events recorded on the launch stream inside the timed region.
     n_batches = max(1, st["batches"])
     roof = None
-    if prog is not None and st["bundle_launches"] and st["bundle_ms"] > 0:
+    if prog is not None and st["bundle_launches"] and st["bundle_ms"] > 0 and not args.partitioned:
         cnt = corc.count_bfs(prog, tab, host_items, threads=threads)
         b_alg = 25 * args.batch + 8 * cnt["rows"] + 4 * cnt["edges"]
         ms_a = st["bundle_ms"] / st["bundle_launches"]
@@ -193,7 +218,7 @@ def main():
     cpu = None
     agree = None
     disagree = []
-    if rank == 0 and world == 1 and not args.no_cpu and prog is not None:
+    if rank == 0 and world == 1 and not args.no_cpu and prog is not None and not args.partitioned:
         t0 = time.perf_counter()
         corc.check(prog, tab, host_items, threads=threads)
         per_batch = time.perf_counter() - t0
@@ -234,6 +259,10 @@ def main():
                          f"1B-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads), "
                          f"{dt:.1f}s; every sampled check compared with the GPU result"}
 
+    if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
+        cp, ce, _ = corc.check(prog, tab, host_items, threads=threads)
+        agree = float(((cp == res) & (ce == errs)).mean())
+
     if rank == 0:
         line = {
             "metric": "permission checks/sec (whole node) at batch 64K, 1B tuples",
@@ -241,9 +270,13 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (tests/synth.py, seed 20251003): deep nested groups, 25 layers, Pareto(2.1) group sizes",
-            "config": {"workload": "config4-deep-nested-groups-replicated", "tuples": n_tuples,
+            "config": {"workload": "config4-deep-nested-groups-" + ("partitioned" if args.partitioned else "replicated"),
+                       "tuples": n_tuples,
                        "batch_per_gpu": args.batch, "users": G.n_users, "groups": G.n_groups,
-                       "docs": G.n_docs, "parallelism": f"batch-sharded x{world}, graph replicated",
+                       "docs": G.n_docs,
+                       "parallelism": (f"graph partitioned x{world} by resource id, per-level all-to-all "
+                                       f"({args.part_backend}), global batch {args.batch * world}")
+                       if args.partitioned else f"batch-sharded x{world}, graph replicated",
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
             "roofline": roof, "cpu_baseline": cpu,
             "oracle_agreement": agree,

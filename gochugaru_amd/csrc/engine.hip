@@ -80,7 +80,10 @@ struct DeviceSnapshot {
   uint32_t* cav_row = nullptr;    // per caveat instance (Engine::caveat_row)
 };
 
+struct PartState;  // partition.inc
+
 struct Workspace {
+  PartState* part = nullptr;  // partitioned batch in progress (partition.inc)
   size_t max_batch = 0, frontier_cap = 0, seg_cap = 0, query_cap = 0, join_cap = 0;
   uint64_t visited_cap = 0;
   DevCheck* checks = nullptr;
@@ -153,6 +156,12 @@ struct Ctx {
   const uint8_t* cav_dyn;
   const gck_item* ck_items;  // the launch's items: check k's context slot
   uint32_t n_ctx;
+  // partitioned graphs (partition.inc): entries for objects another rank owns go to its outbox
+  // region [d * out_cap, (d + 1) * out_cap) instead of the next frontier
+  uint32_t rank, world;
+  Entry* outbox;
+  unsigned* out_cnt;
+  uint32_t out_cap;
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -210,7 +219,21 @@ __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t ob
                                            uint32_t depth, uint32_t cond) {
   if (cond && vlookup(c, make_key(c, q, node, 0, obj))) return;  // unconditional visit exists
   if (vinsert(c, make_key(c, q, node, cond, obj)) <= 0) return;
-  unsigned idx = atomicAdd(&c.ctr->next_size, 1u);
+  Entry* dst = c.next;
+  unsigned idx;
+  if (c.world > 1 && part_owner(obj, c.world) != c.rank) {
+    // another rank owns obj's rows: exchanged after this level (the visited key above also
+    // stops this rank from sending the same entry twice)
+    const uint32_t d = part_owner(obj, c.world);
+    idx = atomicAdd(&c.out_cnt[d], 1u);
+    if (idx >= c.out_cap) {
+      atomicOr(&c.ctr->overflow, 2u);
+      return;
+    }
+    dst = c.outbox + (size_t)d * c.out_cap;
+  } else {
+    idx = atomicAdd(&c.ctr->next_size, 1u);
+  }
   if (idx >= c.frontier_cap) {
     atomicOr(&c.ctr->overflow, 2u);
     return;
@@ -221,7 +244,7 @@ __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t ob
   e.node = node;
   e.depth = (uint8_t)(depth > 255 ? 255 : depth);
   e.cond = (uint8_t)cond;
-  c.next[idx] = e;
+  dst[idx] = e;
   c.queries[q].last_alive = c.level + 1;  // benign race: every writer stores the same value
 }
 
@@ -895,6 +918,9 @@ static void free_list(std::vector<void*>& list) {
   list.clear();
 }
 
+static void free_part(PartState* p);  // partition.inc
+static void partition_filter(const Engine& e, DeviceSnapshot& ds, DevCSR& d, uint64_t& ne);
+
 void device_free(Engine& e) {
   if (e.dev) {
     (void)hipSetDevice(e.device);
@@ -905,6 +931,7 @@ void device_free(Engine& e) {
   if (e.ws) {
     (void)hipSetDevice(e.device);
     Workspace* w = e.ws;
+    free_part(w->part);
     free_list(w->allocs);
     if (w->h_ctr) (void)hipHostFree(w->h_ctr);
     if (w->h_bctrs) (void)hipHostFree(w->h_bctrs);
@@ -1014,6 +1041,10 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
         }
         d.cav = cav;
         d.exp_us = ex;
+      }
+      if (e.part_world > 1) {  // partitioned graph: keep the rows this rank owns (partition.inc)
+        partition_filter(e, *ds, d, ne);
+        b.n_edges = ne;
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
@@ -1533,6 +1564,19 @@ void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_u
     pos += len;
   }
   e.stats.kernel_ms = ms;
+}
+
+#include "partition.inc"
+
+static PartState& part_state(Workspace& w) {
+  if (!w.part) w.part = new PartState();
+  return *w.part;
+}
+
+static void free_part(PartState* p) {
+  if (!p) return;
+  if (p->h_out) (void)hipHostFree(p->h_out);
+  delete p;  // outbox / out_cnt are in the workspace's allocation list
 }
 
 #include "delta.inc"

@@ -136,6 +136,7 @@ struct Workspace;       // engine.hip
 struct Engine {
   gck_config cfg{};
   int device = 0;
+  uint32_t part_rank = 0, part_world = 1;  // partitioned graph (gck_set_partition)
   bool device_ready = false;
   std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
   std::unique_ptr<Schema> schema;
@@ -184,6 +185,13 @@ void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
                        uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
 uint64_t device_bytes(const Engine& e);
+// partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
+void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
+void part_expand(Engine& e, uint64_t* send_counts);
+void part_pack(Engine& e, void* d_send, size_t send_cap);
+void part_ingest(Engine& e, const void* d_recv, size_t n_recv, void* d_flags);
+uint32_t part_resolve(Engine& e, const void* d_flags);
+void part_finish(Engine& e, uint8_t* d_perm, int32_t* d_err);
 void device_free(Engine& e);
 
 }  // namespace gck

@@ -415,7 +415,14 @@ static void apply_updates(Engine& e, uint64_t revision, const std::vector<gck_up
   REQUIRE(revision > e.revision || (ups.empty() && revision == e.revision), GCK_E_REVISION,
           "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
               std::to_string(e.revision));
-  std::vector<UpdateGroup> groups = group_updates(e, ups);
+  std::vector<gck_update> mine;
+  const std::vector<gck_update>* use = &ups;
+  if (e.part_world > 1) {  // partitioned graph: this rank keeps the rows it owns
+    for (const gck_update& u : ups)
+      if (part_owner(u.tuple.resource_id, e.part_world) == e.part_rank) mine.push_back(u);
+    use = &mine;
+  }
+  std::vector<UpdateGroup> groups = group_updates(e, *use);
   if (!groups.empty()) {
     try {
       device_apply(e, groups);
@@ -481,6 +488,7 @@ int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item
     REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
     REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
     REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
+    REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
     check_consistency(e, cs);
     if (n == 0) return;  // empty request -> empty response (client/client_test.go:203-207)
     for (size_t i = 0; i < n; ++i)
@@ -507,6 +515,7 @@ int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n,
     REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
     REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
     REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
+    REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
     if (n == 0) return;
     const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
     device_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream, table, (uint32_t)n_contexts);
@@ -516,6 +525,76 @@ int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n,
 int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us,
                           uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
   return gck_check_bulk_device_ctx(ge, d_items, n, nullptr, nullptr, 0, now_us, d_out_perm, d_out_err, stream);
+}
+
+int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(world >= 1 && world <= 63 && rank < world, GCK_E_INVALID_ARGUMENT, "bad rank / world");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(!e.committed && !e.dev && !e.ws, GCK_E_STATE, "gck_set_partition must precede the first snapshot");
+    e.part_rank = rank;
+    e.part_world = world;
+    if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR;  // both need the whole graph
+  });
+}
+
+uint32_t gck_partition_owner(uint32_t object_id, uint32_t world) {
+  return world <= 1 ? 0u : part_owner(object_id, world);
+}
+
+int gck_part_begin(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(n == 0 || d_items, GCK_E_INVALID_ARGUMENT, "null items");
+    part_begin(e, d_items, n, now_us, stream);
+  });
+}
+
+int gck_part_expand(gck_engine* ge, uint64_t* send_counts) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(send_counts, GCK_E_INVALID_ARGUMENT, "null counts");
+    part_expand(e, send_counts);
+  });
+}
+
+int gck_part_pack(gck_engine* ge, void* d_send, size_t send_cap) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(d_send || !send_cap, GCK_E_INVALID_ARGUMENT, "null buffer");
+    part_pack(e, d_send, send_cap);
+  });
+}
+
+int gck_part_ingest(gck_engine* ge, const void* d_recv, size_t n_recv, void* d_flags) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(d_flags && (d_recv || !n_recv), GCK_E_INVALID_ARGUMENT, "null buffers");
+    part_ingest(e, d_recv, n_recv, d_flags);
+  });
+}
+
+int gck_part_resolve(gck_engine* ge, const void* d_flags, uint32_t* out_active) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(d_flags && out_active, GCK_E_INVALID_ARGUMENT, "null argument");
+    *out_active = part_resolve(e, d_flags);
+  });
+}
+
+int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    part_finish(e, d_out_perm, d_out_err);
+  });
 }
 
 int gck_last_stats(gck_engine* ge, gck_stats* out) {

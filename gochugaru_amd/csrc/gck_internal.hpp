@@ -10,7 +10,22 @@
 #pragma once
 #include <cstdint>
 
+#if defined(__HIPCC__)
+#define GCK_HD __host__ __device__
+#else
+#define GCK_HD
+#endif
+
 namespace gck {
+
+// Partitioned graphs (partition.inc): the rank that owns object `obj` (its CSR
+// rows, its frontier entries). Type-independent, so an object id means the same owner in every
+// relation; a multiplicative hash spreads consecutive ids.
+GCK_HD inline uint32_t part_owner(uint32_t obj, uint32_t world) {
+  uint32_t h = obj * 2654435761u;
+  h ^= h >> 16;
+  return h % world;
+}
 
 constexpr uint16_t kEllipsis = 0xFFFFu;
 constexpr uint32_t kWildcard = 0xFFFFFFFFu;

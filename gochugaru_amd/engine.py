@@ -156,6 +156,14 @@ _SIGS = {
     "gck_check_bulk_device_ctx": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
                                             C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
+    "gck_set_partition": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "gck_partition_owner": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+    "gck_part_begin": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P]),
+    "gck_part_expand": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_part_pack": (C.c_int, [_P, _P, C.c_size_t]),
+    "gck_part_ingest": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "gck_part_resolve": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
+    "gck_part_finish": (C.c_int, [_P, _P, _P]),
     "gck_reset_stats": (C.c_int, [_P]),
 }
 
@@ -223,6 +231,7 @@ class Engine:
         self._lib = lib
         self._type_ids = {}
         self._rel_ids = {}
+        self.part_rank, self.part_world = 0, 1
 
     def close(self):
         if self._h:
@@ -408,6 +417,33 @@ class Engine:
         _check(self._lib.gck_check_bulk_device_ctx(self._h, d_items, n, ctx_arr, ctx_lens, n_ctx, now_us,
                                                    d_perm, d_err, stream))
 
+    # ---- partitioned graphs (gck_part_*; driven by gochugaru_amd.partition) -----------------
+    def set_partition(self, rank: int, world: int):
+        _check(self._lib.gck_set_partition(self._h, rank, world))
+        self.part_rank, self.part_world = rank, world
+
+    def part_begin(self, d_items: int, n: int, now_us: int = 0, stream: Optional[int] = None):
+        _check(self._lib.gck_part_begin(self._h, d_items, n, now_us, stream))
+
+    def part_expand(self) -> np.ndarray:
+        counts = np.zeros(self.part_world, dtype=np.uint64)
+        _check(self._lib.gck_part_expand(self._h, counts.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return counts
+
+    def part_pack(self, d_send: int, cap_entries: int):
+        _check(self._lib.gck_part_pack(self._h, d_send, cap_entries))
+
+    def part_ingest(self, d_recv: int, n_recv: int, d_flags: int):
+        _check(self._lib.gck_part_ingest(self._h, d_recv, n_recv, d_flags))
+
+    def part_resolve(self, d_flags: int) -> int:
+        out = C.c_uint32()
+        _check(self._lib.gck_part_resolve(self._h, d_flags, C.byref(out)))
+        return out.value
+
+    def part_finish(self, d_perm: int, d_err: int):
+        _check(self._lib.gck_part_finish(self._h, d_perm, d_err))
+
     def stats(self) -> Stats:
         s = _Stats()
         _check(self._lib.gck_last_stats(self._h, C.byref(s)))
@@ -483,3 +519,15 @@ def _context_arrays(contexts):
     arr = (C.c_char_p * len(enc))(*enc)
     lens = (C.c_size_t * len(enc))(*[len(b) for b in enc])
     return arr, lens, len(enc)
+
+
+PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES
+
+
+def part_flag_bytes(n: int) -> int:
+    """GCK_PART_FLAG_BYTES(n)."""
+    return 4 * n + 1
+
+
+def partition_owner(object_id: int, world: int) -> int:
+    return load_library().gck_partition_owner(object_id, world)

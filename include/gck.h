@@ -274,6 +274,35 @@ int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
 
+/* ---- partitioned graphs (graphs above one GPU's 288 GB) ----------------
+ * Rank r of `world` keeps the rows of the objects it owns (gck_partition_owner) and checks a
+ * global batch together with the other ranks, one BFS level per round:
+ *
+ *   gck_part_begin(items)                           every rank, the same device items
+ *   loop:
+ *     gck_part_expand(counts[world])                expands the level; entries owed to each rank
+ *     gck_part_pack(send, cap)                      those entries, grouped by rank (cap: entries)
+ *     (caller) all-to-all of counts, then of the entries (GCK_PART_ENTRY_BYTES each)
+ *     gck_part_ingest(recv, n_recv, flags)          flags: GCK_PART_FLAG_BYTES(n) device bytes
+ *     (caller) all-reduce MAX of the flag bytes, in place
+ *     gck_part_resolve(flags, &active)              identical `active` on every rank; 0 = done
+ *   gck_part_finish(perm, err)                      every rank gets every result
+ *
+ * The caller owns the exchange (RCCL all_to_all / all_reduce over xGMI, or any transport).
+ * Union schemas only (no &, -, all()); check-time caveat contexts are not taken. A partitioned
+ * engine refuses gck_check_bulk*. */
+#define GCK_PART_ENTRY_BYTES 12
+#define GCK_PART_FLAG_BYTES(n) (4 * (size_t)(n) + 1)
+/* Before the first snapshot: this engine is rank `rank` of `world` (1 = not partitioned). */
+int gck_set_partition(gck_engine* e, uint32_t rank, uint32_t world);
+uint32_t gck_partition_owner(uint32_t object_id, uint32_t world);
+int gck_part_begin(gck_engine* e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
+int gck_part_expand(gck_engine* e, uint64_t* send_counts);
+int gck_part_pack(gck_engine* e, void* d_send, size_t send_cap);
+int gck_part_ingest(gck_engine* e, const void* d_recv, size_t n_recv, void* d_flags);
+int gck_part_resolve(gck_engine* e, const void* d_flags, uint32_t* out_active);
+int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
+
 #ifdef __cplusplus
 }
 #endif
