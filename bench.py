@@ -61,7 +61,63 @@ def parse():
                          "global batch (batch x ranks) with a per-level all-to-all (gochugaru_amd/partition.py)")
     ap.add_argument("--part-backend", default="nccl", help="exchange backend in --partitioned mode (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank on cuda:0 (a one-GPU rehearsal with gloo)")
+    ap.add_argument("--config", default="nested", choices=["nested", "gdocs", "github"],
+                    help="nested = BASELINE config 4 (the headline, default); gdocs / github = configs 2 / 3 "
+                         "(tests/synth_configs.py) at --scale")
+    ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     return ap.parse_args()
+
+
+class Workload:
+    """One benchmark graph: schema, CSRs in the engine's id space, a check generator and the C
+    oracle's view of the same arrays."""
+
+    def __init__(self, args, dev):
+        import torch
+        from oracle import corc
+        from oracle import spicedb_ref as ref
+        self.kind = args.config
+        if args.config == "nested":
+            from tests import synth
+            G = self.G = synth.build(args.tuples, device=dev)
+            self.schema = synth.SCHEMA
+            self.reserve = [(synth.T_USER, G.n_users), (synth.T_GROUP, G.n_groups), (synth.T_DOC, G.n_docs)]
+            self.csrs = G.csrs()
+            self.union_only = True
+            self.data = "synthetic (tests/synth.py, seed 20251003): deep nested groups, 25 layers, Pareto(2.1) group sizes"
+            self.cfg = {"workload": "config4-deep-nested-groups-" + ("partitioned" if args.partitioned else "replicated"),
+                        "users": G.n_users, "groups": G.n_groups, "docs": G.n_docs}
+            self._checks = lambda n, seed: synth.checks(G, n, seed=seed)
+
+            def oracle():
+                H = synth.host_arrays(G)
+                ids = corc.Ids(ref.Schema(synth.SCHEMA))
+                idx = {(synth.R_MEMBER, synth.T_USER, synth.ELLIPSIS, False): 0,
+                       (synth.R_MEMBER, synth.T_GROUP, synth.R_MEMBER, False): 1,
+                       (synth.R_VIEWER, synth.T_GROUP, synth.R_MEMBER, False): 2}
+                tab = corc.make_csr_table([(H["mem_user_off"], H["mem_user_nbr"], None, None, G.n_groups),
+                                           (H["mem_group_off"], H["mem_group_nbr"], None, None, G.n_groups),
+                                           (H["viewer_off"], H["viewer_nbr"], None, None, G.n_docs)])
+                return corc.encode_program(ids, idx), tab
+            self.oracle = oracle
+        else:
+            from tests import synth_configs
+            W = synth_configs.CONFIGS[args.config](args.scale, device=dev)
+            self.schema = W.schema
+            self.reserve = [(W.t(t), n) for t, n in W.counts.items()]
+            self.csrs = W.csrs
+            self.union_only = args.config == "gdocs"
+            self.data = (f"synthetic (tests/synth_configs.py {args.config}, seed 20251003, scale {args.scale}): "
+                         + ("Google-Docs schema, nested groups, folder forest, parent arrows, public docs"
+                            if args.config == "gdocs" else
+                            "GitHub schema, nested teams, exclusion (banned), intersection and all() over org membership"))
+            self.cfg = {"workload": W.name, **{k + "s": v for k, v in W.counts.items()}}
+            self._checks = lambda n, seed: synth_configs.checks(W, n, seed=seed)
+            self.oracle = W.oracle
+        torch.cuda.synchronize()
+
+    def checks(self, n, seed):
+        return self._checks(n, seed)
 
 
 def main():
@@ -81,11 +137,9 @@ def main():
     dev = torch.device("cuda", local)
 
     from gochugaru_amd.engine import Engine
-    from tests import synth
 
     t0 = time.time()
-    G = synth.build(args.tuples, device=dev)
-    torch.cuda.synchronize()
+    WL = Workload(args, dev)
     t_gen = time.time() - t0
 
     t0 = time.time()
@@ -97,15 +151,12 @@ def main():
                  giant_stage=not args.no_giant, bidir=not args.no_bidir, bidir_both=args.bidir_both)
     if args.partitioned:
         eng.set_partition(rank, world)
-    eng.load_schema(synth.SCHEMA)
-    assert eng.type_id("user") == synth.T_USER and eng.type_id("doc") == synth.T_DOC
-    assert eng.relation_id(synth.T_DOC, "view") == synth.R_VIEW
-    eng.reserve_objects(synth.T_USER, G.n_users)
-    eng.reserve_objects(synth.T_GROUP, G.n_groups)
-    eng.reserve_objects(synth.T_DOC, G.n_docs)
+    eng.load_schema(WL.schema)
+    for t, n in WL.reserve:
+        eng.reserve_objects(t, n)
     eng.begin_snapshot(1)
     keep = []
-    for rel, st, sr, n_rows, off, nbr in G.csrs():
+    for rel, st, sr, n_rows, off, nbr in WL.csrs:
         off32 = off.to(torch.int32).contiguous()
         nbr32 = nbr.contiguous()
         keep.append((off32, nbr32))
@@ -121,14 +172,14 @@ def main():
         # one global batch: every rank's 64K checks, the same items on every rank
         from gochugaru_amd.partition import PartitionedChecker
         pc = PartitionedChecker(eng)
-        items = torch.cat([synth.checks(G, args.batch, seed=1000 + r) for r in range(world)])
+        items = torch.cat([WL.checks(args.batch, 1000 + r) for r in range(world)])
         n_global = args.batch * world
         out = {}
 
         def step():
             out["perm"], out["err"] = pc.check(items, n_global)
     else:
-        items = synth.checks(G, args.batch, seed=1000 + rank)
+        items = WL.checks(args.batch, 1000 + rank)
         perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
         err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
 
@@ -166,20 +217,11 @@ def main():
     errs = err.cpu().numpy()
 
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
-    H = prog = tab = None
+    prog = tab = None
     if rank == 0 and not args.no_oracle:
         from oracle import corc
-        from oracle import spicedb_ref as ref
 
-        H = synth.host_arrays(G)
-        ids = corc.Ids(ref.Schema(synth.SCHEMA))
-        idx = {(synth.R_MEMBER, synth.T_USER, synth.ELLIPSIS, False): 0,
-               (synth.R_MEMBER, synth.T_GROUP, synth.R_MEMBER, False): 1,
-               (synth.R_VIEWER, synth.T_GROUP, synth.R_MEMBER, False): 2}
-        prog = corc.encode_program(ids, idx)
-        tab = corc.make_csr_table([(H["mem_user_off"], H["mem_user_nbr"], None, None, G.n_groups),
-                                   (H["mem_group_off"], H["mem_group_nbr"], None, None, G.n_groups),
-                                   (H["viewer_off"], H["viewer_nbr"], None, None, G.n_docs)])
+        prog, tab = WL.oracle()
         host_items = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
 
@@ -193,14 +235,17 @@ def main():
     n_batches = max(1, st["batches"])
     roof = None
     if prog is not None and st["bundle_launches"] and st["bundle_ms"] > 0 and not args.partitioned:
-        cnt = corc.count_bfs(prog, tab, host_items, threads=threads)
+        if WL.union_only:
+            cnt = corc.count_bfs(prog, tab, host_items, threads=threads)
+        else:  # joins: the recursive oracle's own row / edge counts (memoised per check)
+            cnt = corc.check(prog, tab, host_items, threads=threads)[2]
         b_alg = 25 * args.batch + 8 * cnt["rows"] + 4 * cnt["edges"]
         ms_a = st["bundle_ms"] / st["bundle_launches"]
         ms_b = st["giant_ms"] / st["bundle_launches"]
         ms = ms_a + ms_b
         achieved = b_alg / (ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
-        if args.traffic_json and os.path.exists(args.traffic_json):
+        if args.traffic_json and os.path.exists(args.traffic_json) and WL.kind == "nested":
             tj = json.load(open(args.traffic_json))
             traffic, traffic_src = tj.get("hbm_bytes_per_batch"), args.traffic_json
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -225,7 +270,7 @@ def main():
         extra = int(max(0, min(args.cpu_max_batches, args.cpu_seconds / max(per_batch, 1e-6))) - 1)
         batches = [(items, perm.clone(), err.clone())]
         for k in range(extra):
-            it = synth.checks(G, args.batch, seed=5000 + k)
+            it = WL.checks(args.batch, 5000 + k)
             pk = torch.zeros_like(perm)
             ek = torch.zeros_like(err)
             eng.check_bulk_device(it.data_ptr(), args.batch, pk.data_ptr(), ek.data_ptr(), stream=stream)
@@ -265,15 +310,13 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "permission checks/sec (whole node) at batch 64K, 1B tuples",
+            "metric": ("permission checks/sec (whole node) at batch 64K, 1B tuples" if WL.kind == "nested" else
+                       f"permission checks/sec (whole node) at batch 64K, {WL.cfg['workload']}"),
             "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (tests/synth.py, seed 20251003): deep nested groups, 25 layers, Pareto(2.1) group sizes",
-            "config": {"workload": "config4-deep-nested-groups-" + ("partitioned" if args.partitioned else "replicated"),
-                       "tuples": n_tuples,
-                       "batch_per_gpu": args.batch, "users": G.n_users, "groups": G.n_groups,
-                       "docs": G.n_docs,
+            "data": WL.data,
+            "config": {**WL.cfg, "tuples": n_tuples, "batch_per_gpu": args.batch,
                        "parallelism": (f"graph partitioned x{world} by resource id, per-level all-to-all "
                                        f"({args.part_backend}), global batch {args.batch * world}")
                        if args.partitioned else f"batch-sharded x{world}, graph replicated",
