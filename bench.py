@@ -61,9 +61,11 @@ def parse():
                          "global batch (batch x ranks) with a per-level all-to-all (gochugaru_amd/partition.py)")
     ap.add_argument("--part-backend", default="nccl", help="exchange backend in --partitioned mode (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank on cuda:0 (a one-GPU rehearsal with gloo)")
-    ap.add_argument("--config", default="nested", choices=["nested", "gdocs", "github"],
+    ap.add_argument("--config", default="nested", choices=["nested", "gdocs", "github", "mixed"],
                     help="nested = BASELINE config 4 (the headline, default); gdocs / github = configs 2 / 3 "
-                         "(tests/synth_configs.py) at --scale")
+                         "(tests/synth_configs.py) at --scale; mixed = config 5 (config 2 + 10 %% caveated "
+                         "tuples, check contexts, one Watch batch of --churn x tuples applied per step)")
+    ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     return ap.parse_args()
 
@@ -100,6 +102,21 @@ class Workload:
                                            (H["viewer_off"], H["viewer_nbr"], None, None, G.n_docs)])
                 return corc.encode_program(ids, idx), tab
             self.oracle = oracle
+        elif args.config == "mixed":
+            from tests import synth_configs
+            M = self.M = synth_configs.Mixed(args.scale, device=dev)
+            W = M.W
+            self.schema = W.schema
+            self.reserve = [(W.t(t), n) for t, n in W.counts.items()]
+            self.csrs = None
+            self.union_only = True
+            self.data = (f"synthetic (tests/synth_configs.py Mixed, seed 20251003, scale {args.scale}): config-2 graph, "
+                         f"10% of folder/doc viewer+editor user tuples with only_on_tuesday; checks 25% tuesday / "
+                         f"25% monday / 50% no context; each step applies one Watch batch of {args.churn:.2%} of the "
+                         f"tuples (CREATE/TOUCH/DELETE 45/45/10) before its check batch")
+            self.cfg = {"workload": W.name, **{k + "s": v for k, v in W.counts.items()}}
+            self._checks = lambda n, seed: M.checks(n, seed)
+            self.oracle = None
         else:
             from tests import synth_configs
             W = synth_configs.CONFIGS[args.config](args.scale, device=dev)
@@ -118,6 +135,23 @@ class Workload:
 
     def checks(self, n, seed):
         return self._checks(n, seed)
+
+    def load(self, eng, keep):
+        import torch
+        for t, n in self.reserve:
+            eng.reserve_objects(t, n)
+
+        def loader(rel, st, sr, n_rows, off, nbr):
+            off32 = off.to(torch.int32).contiguous()
+            nbr32 = nbr.contiguous()
+            keep.append((off32, nbr32))
+            eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr32.data_ptr(), nbr32.numel(), device=True)
+        if self.kind == "mixed":
+            self.cav = eng.add_caveat_instance("only_on_tuesday", "")
+            self.M.load(eng, loader, self.cav)
+        else:
+            for c in self.csrs:
+                loader(*c)
 
 
 def main():
@@ -152,15 +186,9 @@ def main():
     if args.partitioned:
         eng.set_partition(rank, world)
     eng.load_schema(WL.schema)
-    for t, n in WL.reserve:
-        eng.reserve_objects(t, n)
     eng.begin_snapshot(1)
     keep = []
-    for rel, st, sr, n_rows, off, nbr in WL.csrs:
-        off32 = off.to(torch.int32).contiguous()
-        nbr32 = nbr.contiguous()
-        keep.append((off32, nbr32))
-        eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr32.data_ptr(), nbr32.numel(), device=True)
+    WL.load(eng, keep)
     torch.cuda.synchronize()
     eng.commit_snapshot()
     t_load = time.time() - t0
@@ -178,6 +206,25 @@ def main():
 
         def step():
             out["perm"], out["err"] = pc.check(items, n_global)
+    elif WL.kind == "mixed":
+        # config 5: per step one Watch batch (pre-generated: the stream's arrivals) then one check
+        # batch with contexts, at the revision the batch moved the snapshot to
+        from tests.synth_configs import CONTEXTS
+        items = WL.checks(args.batch, 1000 + rank)
+        perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
+        err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+        n_up = max(1, int(n_tuples * args.churn))
+        batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warmup + args.steps)]
+        rev = {"r": 1, "k": 0, "apply_s": 0.0}
+
+        def step():
+            t_a = time.perf_counter()
+            rev["r"] += 1
+            eng.apply_updates(rev["r"], batches[rev["k"]])
+            rev["k"] += 1
+            rev["apply_s"] += time.perf_counter() - t_a
+            eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream,
+                                  contexts=CONTEXTS)
     else:
         items = WL.checks(args.batch, 1000 + rank)
         perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
@@ -218,7 +265,12 @@ def main():
 
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
     prog = tab = None
-    if rank == 0 and not args.no_oracle:
+    if rank == 0 and not args.no_oracle and WL.kind == "mixed":
+        from oracle import corc  # the final snapshot (after every Watch batch) vs the timed batch
+        hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+        cp, ce = WL.M.expected(hi, threads=args.cpu_threads or min(16, os.cpu_count() or 1))
+        agree_mixed = float(((cp == res) & (ce == errs)).mean())
+    if rank == 0 and not args.no_oracle and WL.kind != "mixed":
         from oracle import corc
 
         prog, tab = WL.oracle()
@@ -304,6 +356,9 @@ def main():
                          f"1B-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads), "
                          f"{dt:.1f}s; every sampled check compared with the GPU result"}
 
+    if rank == 0 and WL.kind == "mixed" and not args.no_oracle:
+        agree = agree_mixed
+
     if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
         cp, ce, _ = corc.check(prog, tab, host_items, threads=threads)
         agree = float(((cp == res) & (ce == errs)).mean())
@@ -336,6 +391,8 @@ def main():
                        "giant_ms_per_batch": round(st["giant_ms"] / n_batches, 4),
                        "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
+            **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warmup + args.steps) * 1e3, 3),
+                          "revision": rev["r"]}} if WL.kind == "mixed" else {}),
         }
         print(json.dumps(line), flush=True)
     eng.close()

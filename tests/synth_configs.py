@@ -232,3 +232,183 @@ def checks(W: Workload, n: int = 65536, seed: int = 7) -> torch.Tensor:
 
 
 CONFIGS = {"gdocs": gdocs, "github": github}
+
+
+# ---- config 5: caveats + Watch churn ---------------------------------------------------------
+
+MIXED_SCHEMA = """
+caveat only_on_tuesday(day_of_the_week string) {
+  day_of_the_week == "tuesday"
+}
+definition user {}
+definition group {
+  relation member: user | group#member
+}
+definition folder {
+  relation parent: folder
+  relation viewer: user | group#member | user with only_on_tuesday
+  relation editor: user | group#member | user with only_on_tuesday
+  permission edit = editor + parent->edit
+  permission view = viewer + edit + parent->view
+}
+definition doc {
+  relation parent: folder
+  relation owner: user
+  relation viewer: user | user:* | group#member | user with only_on_tuesday
+  relation editor: user | group#member | user with only_on_tuesday
+  permission edit = owner + editor + parent->edit
+  permission view = viewer + edit + parent->view
+}
+"""
+
+CONTEXTS = ['{"day_of_the_week":"tuesday"}', '{"day_of_the_week":"monday"}']  # context slots 1, 2
+CHURN_KINDS = [("folder", "viewer"), ("folder", "editor"), ("doc", "viewer"), ("doc", "editor")]
+
+
+class Mixed:
+    """BASELINE.json config 5: the config-2 graph with 10 % of the folder / doc viewer and editor
+    user tuples caveated ``with only_on_tuesday``, checks of which half carry a check-time
+    context (tuesday: the caveat holds, monday: it fails) and half none (CONDITIONAL), and Watch
+    churn on those relations (CREATE / TOUCH / DELETE 45 / 45 / 10, TOUCH toggling the caveat).
+
+    The state of the churned user kinds is kept on the host as sorted (object << 32 | subject)
+    keys with a caveat flag, so the expected answers after any number of update batches come
+    from the C oracle over a rebuilt snapshot: caveats can only be true, false or missing here,
+    so the three context classes are three oracle runs (caveated edges plain / absent /
+    CONDITIONAL)."""
+
+    def __init__(self, scale: float = 1.0, seed: int = 20251003, device="cuda", cav_frac: float = 0.1):
+        self.W = W = gdocs(scale, seed, device)
+        W.name, W.schema = "config5-mixed", MIXED_SCHEMA
+        W.ids = corc.Ids(ref.Schema(MIXED_SCHEMA))
+        self.device = device
+        self.rng = np.random.default_rng(seed)
+        self.kinds = [(W.r(t, r), W.t("user"), ELLIPSIS, W.counts[t]) for t, r in CHURN_KINDS]
+        self.static = [c for c in W.csrs if (c[0], c[1], c[2]) not in {k[:3] for k in self.kinds}]
+        self.state = {}  # kind -> (keys u64 sorted, caveated bool)
+        for rid, st, sr, n_rows in self.kinds:
+            off, nbr = W.find(*self._names(rid))[4:6]
+            row = _segment_ids(off, nbr.numel()).cpu().numpy().astype(np.uint64)
+            sid = nbr.cpu().numpy().view(np.uint32).astype(np.uint64)
+            keys = (row << np.uint64(32)) | sid
+            cav = (self.rng.random(keys.size) < cav_frac) & (sid != WILD)
+            self.state[(rid, st, sr)] = (keys, cav)
+
+    def _names(self, rid):
+        t, r = self.W.ids.rels[rid]
+        return t, r, "user"
+
+    # ---- engine ingest ------------------------------------------------------------------------
+    def load(self, eng, plain_csr_loader, cav_instance: int):
+        """Static CSRs and the plain part of the churned kinds through `plain_csr_loader`
+        (gck_load_csr), the caveated part as interned tuples (gck_add_tuples)."""
+        from gochugaru_amd.engine import TUPLE_DTYPE
+        for c in self.static:
+            plain_csr_loader(*c)
+        tups = []
+        for (rid, st, sr), (keys, cav) in self.state.items():
+            n_rows = self.W.counts[self.W.ids.rels[rid][0]]
+            off, nbr = self._csr(keys[~cav], n_rows)
+            plain_csr_loader(rid, st, sr, n_rows, torch.from_numpy(off.astype(np.int64)).to(self.device),
+                             torch.from_numpy(nbr.view(np.int32)).to(self.device))
+            t = np.zeros(int(cav.sum()), dtype=TUPLE_DTYPE)
+            t["resource_type"] = self.W.t(self.W.ids.rels[rid][0])
+            t["relation"] = rid
+            t["resource_id"] = keys[cav] >> np.uint64(32)
+            t["subject_type"] = st
+            t["subject_relation"] = sr
+            t["subject_id"] = keys[cav] & np.uint64(0xFFFFFFFF)
+            t["caveat"] = cav_instance
+            tups.append(t)
+        eng.add_tuples(np.concatenate(tups))
+
+    @staticmethod
+    def _csr(keys, n_rows):
+        row = (keys >> np.uint64(32)).astype(np.int64)
+        off = np.zeros(n_rows + 1, dtype=np.uint32)
+        off[1:] = np.cumsum(np.bincount(row, minlength=n_rows))
+        return off, (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+    # ---- Watch churn ----------------------------------------------------------------------------
+    def churn(self, n: int, cav_instance: int):
+        """One Watch batch of n updates (unique relationships) as UPDATE_DTYPE records, applied
+        to the host state as well."""
+        from gochugaru_amd.engine import UPDATE_CREATE, UPDATE_DELETE, UPDATE_DTYPE, UPDATE_TOUCH
+        rng = self.rng
+        out = []
+        per = np.bincount(rng.integers(0, len(self.kinds), n), minlength=len(self.kinds))
+        for (rid, st, sr, n_rows), k in zip(self.kinds, per):
+            keys, cav = self.state[(rid, st, sr)]
+            ops = rng.choice([UPDATE_CREATE, UPDATE_TOUCH, UPDATE_DELETE], size=k, p=[0.45, 0.45, 0.10])
+            n_new = int((ops == UPDATE_CREATE).sum())
+            new = ((rng.integers(0, n_rows, n_new).astype(np.uint64) << np.uint64(32))
+                   | rng.integers(0, self.W.counts["user"], n_new).astype(np.uint64))
+            old = keys[rng.integers(0, keys.size, k - n_new)] if keys.size else np.zeros(0, np.uint64)
+            ukeys = np.concatenate([new, old])
+            uops = np.concatenate([ops[ops == UPDATE_CREATE], ops[ops != UPDATE_CREATE]])
+            ukeys, first = np.unique(ukeys, return_index=True)
+            uops = uops[first]
+            ucav = rng.random(ukeys.size) < 0.1
+            # TOUCH of an existing key toggles its caveat half of the time
+            pos = np.searchsorted(keys, ukeys)
+            exists = (pos < keys.size) & (keys[np.minimum(pos, max(keys.size - 1, 0))] == ukeys)
+            toggle = (uops == UPDATE_TOUCH) & exists & (rng.random(ukeys.size) < 0.5)
+            ucav = np.where(toggle, ~cav[np.minimum(pos, max(keys.size - 1, 0))], ucav)
+            ucav &= (ukeys & np.uint64(0xFFFFFFFF)) != np.uint64(WILD)  # no caveated wildcard kind
+            # host state: drop every updated key, re-insert the upserts
+            keep = ~np.isin(keys, ukeys)
+            up = uops != UPDATE_DELETE
+            keys2 = np.concatenate([keys[keep], ukeys[up]])
+            cav2 = np.concatenate([cav[keep], ucav[up]])
+            order = np.argsort(keys2, kind="stable")
+            self.state[(rid, st, sr)] = (keys2[order], cav2[order])
+            u = np.zeros(ukeys.size, dtype=UPDATE_DTYPE)
+            u["op"] = uops
+            t = u["tuple"]
+            t["resource_type"] = self.W.t(self.W.ids.rels[rid][0])
+            t["relation"] = rid
+            t["resource_id"] = ukeys >> np.uint64(32)
+            t["subject_type"] = st
+            t["subject_relation"] = sr
+            t["subject_id"] = ukeys & np.uint64(0xFFFFFFFF)
+            t["caveat"] = np.where(ucav & up, cav_instance, 0)
+            u["tuple"] = t
+            out.append(u)
+        return np.concatenate(out)
+
+    # ---- expected answers ------------------------------------------------------------------------
+    def expected(self, items_host: np.ndarray, threads: int = 16):
+        """(perm, err) for items whose context_slot is 0 (none), 1 (tuesday) or 2 (monday)."""
+        res = []
+        for mode in ("cond", "true", "false"):
+            idx, arrays = {}, []
+            for rid, st, sr, n_rows, off, nbr in self.static:
+                idx[(rid, st, sr, False)] = len(arrays)
+                arrays.append((off.to(torch.int64).cpu().numpy().astype(np.uint32),
+                               nbr.cpu().numpy().view(np.uint32), None, None, n_rows))
+            for (rid, st, sr), (keys, cav) in self.state.items():
+                n_rows = self.W.counts[self.W.ids.rels[rid][0]]
+                sel = np.ones(keys.size, bool) if mode == "true" else ~cav
+                off, nbr = self._csr(keys[sel], n_rows)
+                idx[(rid, st, sr, False)] = len(arrays)
+                arrays.append((off, nbr, None, None, n_rows))
+                if mode == "cond" and cav.any():
+                    off, nbr = self._csr(keys[cav], n_rows)
+                    idx[(rid, st, sr, True)] = len(arrays)
+                    arrays.append((off, nbr, np.ones(nbr.size, np.uint32), np.zeros(nbr.size, np.int64), n_rows))
+            prog = corc.encode_program(self.W.ids, idx)
+            res.append(corc.check(prog, corc.make_csr_table(arrays), items_host, threads=threads)[:2])
+        slot = items_host["context_slot"]
+        perm = np.where(slot == 1, res[1][0], np.where(slot == 2, res[2][0], res[0][0]))
+        err = np.where(slot == 1, res[1][1], np.where(slot == 2, res[2][1], res[0][1]))
+        return perm, err
+
+    def checks(self, n: int, seed: int) -> torch.Tensor:
+        """Config-2 checks with context slots: 25 % tuesday, 25 % monday, 50 % none."""
+        items = checks(self.W, n, seed)
+        g = _gen(items.device, seed + 1)
+        slot = torch.floor(torch.rand(n, generator=g, device=items.device) * 4).to(torch.int32).clamp_(max=3)
+        slot = torch.where(slot >= 2, torch.zeros_like(slot), slot + 1)
+        items.view(torch.int32).reshape(n, 5)[:, 4] = slot
+        return items
+
