@@ -934,7 +934,6 @@ void device_free(Engine& e) {
     free_part(w->part);
     free_list(w->allocs);
     if (w->h_ctr) (void)hipHostFree(w->h_ctr);
-    if (w->h_bctrs) (void)hipHostFree(w->h_bctrs);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     if (w->ev2) (void)hipEventDestroy(w->ev2);
@@ -1156,19 +1155,27 @@ static Workspace* ensure_workspace(Engine& e) {
     w->fr[1] = dalloc<Entry>(w->allocs, w->frontier_cap);
     w->segs = dalloc<Segment>(w->allocs, w->seg_cap);
     w->visited = dalloc<unsigned long long>(w->allocs, w->visited_cap);
-    w->ctr = dalloc<DevCounters>(w->allocs, 1);
+    // the level / batch counters and the bundle counters share one buffer (one memset, one copy
+    // back per batch)
+    static_assert(sizeof(DevCounters) % 8 == 0, "bundle counters follow DevCounters");
+    w->ctr = reinterpret_cast<DevCounters*>(dalloc<unsigned char>(w->allocs, sizeof(DevCounters) + 4 * sizeof(unsigned)));
+    w->b_ctrs = reinterpret_cast<unsigned*>(w->ctr + 1);
     w->d_items = dalloc<gck_item>(w->allocs, w->max_batch);
     w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
     w->d_err = dalloc<int32_t>(w->allocs, w->max_batch);
-    HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters) + 4 * sizeof(unsigned), hipHostMallocDefault));
+    w->h_bctrs = reinterpret_cast<unsigned*>(w->h_ctr + 1);
     // bundle path scratch: per resident wavefront, a frontier pair and a visited table
     if (!(cf.flags & GCK_FLAG_NO_BUNDLE)) {
       int cus = 256;
       hipDeviceProp_t prop;
       if (hipGetDeviceProperties(&prop, e.device) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
-      const uint32_t wpc = cf.bundle_waves_per_cu ? cf.bundle_waves_per_cu : 16;
-      w->b_checks = cf.bundle_checks ? std::min<uint32_t>(cf.bundle_checks, kBMax) : 16;
+      // 8 resident bundle waves per CU with 32 checks each: the level latency of this gather-bound
+      // loop grows with the requests in flight, so fewer, fuller waves finish a batch sooner
+      // (config 4 sweep, profiles/r01/sweeps: 16 x 16 -> 250 M/s, 8 x 32 -> 323 M/s)
+      const uint32_t wpc = cf.bundle_waves_per_cu ? cf.bundle_waves_per_cu : 8;
+      w->b_checks = cf.bundle_checks ? std::min<uint32_t>(cf.bundle_checks, kBMax) : 32;
       w->b_fc = cf.bundle_frontier ? cf.bundle_frontier : 4096;
       w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 16384);
       w->b_blocks = std::max<uint32_t>(1, (uint32_t)cus * wpc / kWaves);
@@ -1187,11 +1194,9 @@ static Workspace* ensure_workspace(Engine& e) {
       w->g_vlog = dalloc<uint32_t>(w->allocs, (size_t)w->g_slots * w->g_vslots);
       HIP_OK(hipMemset(w->g_vis, 0, (size_t)w->g_slots * w->g_vslots * sizeof(unsigned long long)));
       w->g_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
-      w->b_ctrs = dalloc<unsigned>(w->allocs, 4);
       w->def_items = dalloc<gck_item>(w->allocs, w->max_batch);
       w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
       w->def_err = dalloc<int32_t>(w->allocs, w->max_batch);
-      HIP_OK(hipHostMalloc(&w->h_bctrs, 4 * sizeof(unsigned), hipHostMallocDefault));
     }
     HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&w->ev0));
@@ -1399,8 +1404,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   g.timing = timing_env ? timing + (size_t)kTimingWords * (n + 1) : nullptr;
   if (timing_env) HIP_OK(hipMemsetAsync(timing, 0, timing_words * 8, st));
   HIP_OK(hipEventRecord(w.ev0, st));
-  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
-  HIP_OK(hipMemsetAsync(w.b_ctrs, 0, 4 * sizeof(unsigned), st));
+  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));  // + b_ctrs
   if (profile) HIP_OK(hipEventRecord(w.pev[0], st));
   // the node program is staged in LDS when it fits (bundle.inc)
   const size_t prog_bytes = (size_t)c.n_csrs * sizeof(DevCSR) + (size_t)c.n_nodes * sizeof(DevNode) +
@@ -1429,8 +1433,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
     HIP_OK(hipGetLastError());
   }
   if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
-  HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(w.h_bctrs, w.b_ctrs, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters) + 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIP_OK(hipEventRecord(w.ev1, st));
   HIP_OK(hipStreamSynchronize(st));
   float ms = 0.f;

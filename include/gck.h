@@ -102,10 +102,10 @@ typedef struct gck_config {
   uint64_t frontier_capacity;  /* entries per frontier buffer; 0 = auto */
   uint64_t segment_capacity;   /* row segments per level; 0 = auto */
   uint64_t query_capacity;     /* queries per batch (checks + sub-queries of joins); 0 = auto */
-  uint32_t bundle_checks;      /* checks per wavefront bundle (1..32); 0 = 16 */
+  uint32_t bundle_checks;      /* checks per wavefront bundle (1..48); 0 = 32 */
   uint32_t bundle_frontier;    /* frontier entries per wavefront; 0 = 4096 */
   uint32_t bundle_visited;     /* visited slots per wavefront (power of 2); 0 = 16384 */
-  uint32_t bundle_waves_per_cu;/* resident wavefronts per CU for the bundle kernel; 0 = 16 */
+  uint32_t bundle_waves_per_cu;/* resident wavefronts per CU for the bundle kernel; 0 = 8 */
   uint32_t bundle_budget;      /* entries one check may push in a wavefront bundle before it is
                                   handed to a 16-wave workgroup; 0 = 1024 */
   uint32_t giant_frontier;     /* frontier entries per 16-wave workgroup bundle; 0 = 65536 */

@@ -171,7 +171,7 @@ PATHS = {
     # grid-wide level-synchronous kernels only
     "wide": {"wide_only": True},
     # tiny per-wave scratch: most bundles overflow and are re-run by the later stages
-    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 16},
+    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 8},
     # tiny work budget: almost every check is handed to a 16-wave workgroup bundle
     "giant": {"bundle_budget": 2},
     # ... and those overflow their workgroup scratch into the grid-wide path
