@@ -896,7 +896,9 @@ template <class T>
 static T* dalloc(std::vector<void*>& list, size_t count, uint64_t* bytes = nullptr) {
   void* p = nullptr;
   size_t sz = std::max<size_t>(count, 1) * sizeof(T);
-  HIP_OK(hipMalloc(&p, sz));
+  // stream-ordered pool (device_init keeps freed blocks cached): a Watch batch replaces a few
+  // CSRs, and hipFree would synchronise the device once per array
+  HIP_OK(hipMallocAsync(&p, sz, nullptr));
   list.push_back(p);
   if (bytes) *bytes += sz;
   return static_cast<T*>(p);
@@ -909,12 +911,18 @@ int device_init(Engine& e) {
     throw Error(GCK_E_NO_DEVICE, "no HIP device available (libgck requires an MI355X)");
   if (e.cfg.device < 0 || e.cfg.device >= n) throw Error(GCK_E_INVALID_ARGUMENT, "bad device ordinal");
   e.device = e.cfg.device;
+  HIP_OK(hipSetDevice(e.device));
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, e.device) == hipSuccess) {
+    uint64_t keep = ~0ull;  // never hand freed blocks back to the driver between batches
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
   e.device_ready = true;
   return 0;
 }
 
 static void free_list(std::vector<void*>& list) {
-  for (void* p : list) (void)hipFree(p);
+  for (void* p : list) (void)hipFreeAsync(p, nullptr);
   list.clear();
 }
 
@@ -922,6 +930,12 @@ static void free_part(PartState* p);  // partition.inc
 static void partition_filter(const Engine& e, DeviceSnapshot& ds, DevCSR& d, uint64_t& ne);
 
 void device_free(Engine& e) {
+  if (e.delta_scratch) {
+    (void)hipSetDevice(e.device);
+    (void)hipFree(e.delta_scratch);
+    e.delta_scratch = nullptr;
+    e.delta_scratch_cap = 0;
+  }
   if (e.dev) {
     (void)hipSetDevice(e.device);
     free_list(e.dev->allocs);
@@ -1128,6 +1142,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     delete e.dev;
   }
   e.dev = ds;
+  HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
 }
 
 static Workspace* ensure_workspace(Engine& e) {
@@ -1203,6 +1218,7 @@ static Workspace* ensure_workspace(Engine& e) {
     HIP_OK(hipEventCreate(&w->ev1));
     HIP_OK(hipEventCreate(&w->ev2));
     for (hipEvent_t& ev : w->pev) HIP_OK(hipEventCreate(&ev));
+    HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
   } catch (...) {
     free_list(w->allocs);
     if (w->h_ctr) (void)hipHostFree(w->h_ctr);
@@ -1524,11 +1540,12 @@ static void stage_caveats(Workspace& w, const std::vector<uint8_t>& table, uint3
     if (w.cav_dyn) {
       HIP_OK(hipStreamSynchronize(st));
       w.allocs.erase(std::remove(w.allocs.begin(), w.allocs.end(), (void*)w.cav_dyn), w.allocs.end());
-      HIP_OK(hipFree(w.cav_dyn));
+      HIP_OK(hipFreeAsync(w.cav_dyn, nullptr));
       w.cav_dyn = nullptr;
     }
     w.cav_dyn_cap = std::max(table.size(), w.cav_dyn_cap * 2);
     w.cav_dyn = dalloc<uint8_t>(w.allocs, w.cav_dyn_cap);
+    HIP_OK(hipStreamSynchronize(nullptr));  // the allocation is ordered on the null stream
   }
   HIP_OK(hipMemcpyAsync(w.cav_dyn, table.data(), table.size(), hipMemcpyHostToDevice, st));
 }

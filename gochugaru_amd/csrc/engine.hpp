@@ -162,6 +162,8 @@ struct Engine {
   DeviceSnapshot* dev = nullptr;
   std::mutex ws_mu;
   Workspace* ws = nullptr;
+  void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
+  size_t delta_scratch_cap = 0;
   gck_stats stats{};
   ~Engine();
 };
