@@ -26,8 +26,9 @@ from . import consistency as _cs
 from . import rel as _rel
 from .consistency import Background, Context, Strategy
 from .engine import (CONSISTENCY_AT_LEAST, CONSISTENCY_FULL, CONSISTENCY_MIN_LATENCY,
-                     CONSISTENCY_SNAPSHOT, GCK_E_DEVICE, GCK_E_REVISION, ITEM_ERROR_MESSAGES,
-                     PERM_HAS, Engine, GckError)
+                     CONSISTENCY_SNAPSHOT, ELLIPSIS, GCK_E_DEVICE, GCK_E_NOT_FOUND, GCK_E_REVISION,
+                     ID_ABSENT, ITEM_ERROR_MESSAGES, PERM_HAS, REL_INVALID, TYPE_INVALID, Engine,
+                     GckError)
 
 CHECK_ITER_CHUNK = 1000  # client/client.go:166
 
@@ -188,6 +189,60 @@ class Client:
         for c in checks:
             yield c, None
         return True
+
+    # ---- lookups (client/client.go:501-599) ------------------------------------------------
+    def LookupResources(self, ctx: Optional[Context], cs: Optional[Strategy], permission: str,
+                        subject: str) -> Iterator[Tuple[str, Optional[Exception]]]:
+        """``client/client.go:508-552``: yields the ids of the objects of ``permission``'s type
+        ("document#reader") on which ``subject`` ("user:jimmy" or "team:admin#member") has the
+        permission (HAS or CONDITIONAL, as SpiceDB streams both); stops at the first error."""
+        self.checkOverlap(ctx)
+        try:
+            subj_type, subj_id, subj_rel = _rel.ParseObjectSet(subject)
+            obj_type, obj_rel = _rel.ParseTypedRelation(permission)
+            requirement, revision = _requirement(cs)
+            eng = self.engine
+            rt = eng.type_id(obj_type)
+            st = eng.type_id(subj_type)
+            perm = eng.relation_id(rt, obj_rel)
+            srel = ELLIPSIS if subj_rel in ("", "...") else eng.relation_id(st, subj_rel)
+            if TYPE_INVALID in (rt, st) or REL_INVALID in (perm, srel):
+                raise GckError(GCK_E_NOT_FOUND, "object definition or relation not found")
+            sid = int(eng.intern(st, [subj_id])[0])  # unknown ids stay ABSENT: wildcards still match
+            ids, _ = retryRetriableErrors(ctx or Background, lambda: eng.lookup_resources(
+                rt, perm, st, srel, sid, requirement, revision))
+            names = [eng.object_name(rt, int(i)) for i in ids]
+        except Exception as e:  # noqa: BLE001 — Go yields ("", err) and stops
+            yield "", e
+            return
+        for n in names:
+            yield n, None
+
+    def LookupSubjects(self, ctx: Optional[Context], cs: Optional[Strategy], resource: str, permission: str,
+                       subject: str) -> Iterator[Tuple[str, Optional[Exception]]]:
+        """``client/client.go:560-599``: yields the ids of the subjects of type ``subject``
+        ("user" or "team#member") that have ``permission`` on ``resource`` ("document:README")."""
+        self.checkOverlap(ctx)
+        try:
+            res_type, res_id, _ = _rel.ParseObjectSet(resource)
+            subj_type, subj_rel, _ = _rel._cut(subject, "#")
+            requirement, revision = _requirement(cs)
+            eng = self.engine
+            rt = eng.type_id(res_type)
+            st = eng.type_id(subj_type)
+            perm = eng.relation_id(rt, permission)
+            srel = ELLIPSIS if subj_rel in ("", "...") else eng.relation_id(st, subj_rel)
+            if TYPE_INVALID in (rt, st) or REL_INVALID in (perm, srel):
+                raise GckError(GCK_E_NOT_FOUND, "object definition or relation not found")
+            rid = int(eng.intern(rt, [res_id])[0])
+            ids, _ = retryRetriableErrors(ctx or Background, lambda: eng.lookup_subjects(
+                rt, rid, perm, st, srel, requirement, revision)) if rid != ID_ABSENT else ([], [])
+            names = [eng.object_name(st, int(i)) for i in ids]
+        except Exception as e:  # noqa: BLE001
+            yield "", e
+            return
+        for n in names:
+            yield n, None
 
     # ---- snapshot plumbing (ReadSchema + ExportRelationships at its revision) -------------
     def LoadSnapshot(self, schema: str, revision: int, relationships: Iterable) -> None:

@@ -123,6 +123,10 @@ struct Workspace {
   uint8_t* cav_dyn = nullptr;
   size_t cav_dyn_cap = 0;
   uint32_t n_ctx = 0;
+  // lookups (lookup.inc): matching ids / permissionships of one candidate chunk, their count
+  uint32_t* lk_ids = nullptr;
+  uint8_t* lk_perm = nullptr;
+  unsigned* lk_cnt = nullptr;
   std::vector<void*> allocs;
 };
 
@@ -1142,6 +1146,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     delete e.dev;
   }
   e.dev = ds;
+  e.generation++;
   HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
 }
 
@@ -1587,6 +1592,7 @@ void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_u
 }
 
 #include "partition.inc"
+#include "lookup.inc"
 
 static PartState& part_state(Workspace& w) {
   if (!w.part) w.part = new PartState();

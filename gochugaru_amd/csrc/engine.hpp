@@ -162,6 +162,7 @@ struct Engine {
   DeviceSnapshot* dev = nullptr;
   std::mutex ws_mu;
   Workspace* ws = nullptr;
+  uint64_t generation = 0;        // bumped by every device snapshot (commit, Watch batch)
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   size_t delta_scratch_cap = 0;
   gck_stats stats{};
@@ -187,6 +188,10 @@ void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
                        uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
 uint64_t device_bytes(const Engine& e);
+// lookups (lookup.inc): candidates [0, n) of the varying id of `proto` (resource id when
+// vary_res, else subject id); matching ids ascending with their permissionship
+void device_lookup(Engine& e, const gck_item& proto, bool vary_res, uint32_t n_candidates, int64_t now_us,
+                   std::vector<uint32_t>& ids, std::vector<uint8_t>& perms);
 // partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
 void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
 void part_expand(Engine& e, uint64_t* send_counts);

@@ -597,6 +597,75 @@ int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
   });
 }
 
+// The result of the last lookup of this thread, so a caller whose buffer was too small gets it
+// on the retry without a second sweep.
+struct LookupCache {
+  const gck_engine* e = nullptr;
+  uint64_t generation = 0;
+  gck_item proto{};
+  bool vary_res = false;
+  int64_t now_us = 0;
+  std::vector<uint32_t> ids;
+  std::vector<uint8_t> perms;
+};
+thread_local LookupCache g_lookup;
+
+static void lookup(gck_engine* ge, const gck_consistency* cs, const gck_item& proto, bool vary_res, int64_t now_us,
+                   uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n) {
+  Engine& e = need(ge);
+  std::shared_lock<std::shared_mutex> lk(e.mu);
+  REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+  REQUIRE(out_n && (cap == 0 || (out_ids && out_perm)), GCK_E_INVALID_ARGUMENT, "null buffers");
+  REQUIRE(e.part_world <= 1, GCK_E_STATE, "lookups are not available on a partitioned engine");
+  check_consistency(e, cs);
+  const Schema& sc = *e.schema;
+  REQUIRE(proto.resource_type < sc.types.size() && proto.subject_type < sc.types.size(), GCK_E_NOT_FOUND,
+          "object definition not found");
+  REQUIRE(proto.permission < sc.rels.size() && sc.rels[proto.permission].type == proto.resource_type,
+          GCK_E_NOT_FOUND, "relation/permission not found");
+  REQUIRE(proto.subject_relation == GCK_ELLIPSIS ||
+              (proto.subject_relation < sc.rels.size() && sc.rels[proto.subject_relation].type == proto.subject_type),
+          GCK_E_NOT_FOUND, "subject relation not found");
+  const bool hit = g_lookup.e == ge && g_lookup.generation == e.generation && g_lookup.vary_res == vary_res &&
+                   g_lookup.now_us == now_us && std::memcmp(&g_lookup.proto, &proto, sizeof(gck_item)) == 0;
+  if (!hit) {
+    g_lookup.e = nullptr;
+    const uint32_t n = e.interner[vary_res ? proto.resource_type : proto.subject_type].count;
+    device_lookup(e, proto, vary_res, n, now_us, g_lookup.ids, g_lookup.perms);
+    g_lookup.e = ge;
+    g_lookup.generation = e.generation;
+    g_lookup.proto = proto;
+    g_lookup.vary_res = vary_res;
+    g_lookup.now_us = now_us;
+  }
+  *out_n = g_lookup.ids.size();
+  REQUIRE(cap >= g_lookup.ids.size(), GCK_E_CAPACITY,
+          "lookup result has " + std::to_string(g_lookup.ids.size()) + " ids: retry with that capacity");
+  if (!g_lookup.ids.empty()) {
+    std::memcpy(out_ids, g_lookup.ids.data(), g_lookup.ids.size() * 4);
+    std::memcpy(out_perm, g_lookup.perms.data(), g_lookup.perms.size());
+  }
+}
+
+int gck_lookup_resources(gck_engine* ge, const gck_consistency* cs, uint16_t resource_type, uint16_t permission,
+                         uint16_t subject_type, uint16_t subject_relation, uint32_t subject_id, int64_t now_us,
+                         uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n) {
+  return guard([&] {
+    REQUIRE(subject_id != GCK_ID_WILDCARD, GCK_E_INVALID_ARGUMENT, "cannot perform lookup on wildcard subject");
+    gck_item proto{resource_type, permission, 0, subject_type, subject_relation, subject_id, 0};
+    lookup(ge, cs, proto, true, now_us, out_ids, out_perm, cap, out_n);
+  });
+}
+
+int gck_lookup_subjects(gck_engine* ge, const gck_consistency* cs, uint16_t resource_type, uint32_t resource_id,
+                        uint16_t permission, uint16_t subject_type, uint16_t subject_relation, int64_t now_us,
+                        uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n) {
+  return guard([&] {
+    gck_item proto{resource_type, permission, resource_id, subject_type, subject_relation, 0, 0};
+    lookup(ge, cs, proto, false, now_us, out_ids, out_perm, cap, out_n);
+  });
+}
+
 int gck_last_stats(gck_engine* ge, gck_stats* out) {
   return guard([&] {
     Engine& e = need(ge);

@@ -156,6 +156,12 @@ _SIGS = {
     "gck_check_bulk_device_ctx": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
                                             C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
+    "gck_lookup_resources": (C.c_int, [_P, C.POINTER(_Consistency), C.c_uint16, C.c_uint16, C.c_uint16,
+                                       C.c_uint16, C.c_uint32, C.c_int64, _P, _P, C.c_size_t,
+                                       C.POINTER(C.c_size_t)]),
+    "gck_lookup_subjects": (C.c_int, [_P, C.POINTER(_Consistency), C.c_uint16, C.c_uint32, C.c_uint16,
+                                      C.c_uint16, C.c_uint16, C.c_int64, _P, _P, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]),
     "gck_set_partition": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "gck_partition_owner": (C.c_uint32, [C.c_uint32, C.c_uint32]),
     "gck_part_begin": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P]),
@@ -416,6 +422,38 @@ class Engine:
         ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
         _check(self._lib.gck_check_bulk_device_ctx(self._h, d_items, n, ctx_arr, ctx_lens, n_ctx, now_us,
                                                    d_perm, d_err, stream))
+
+    # ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) --------
+    def _lookup(self, fn, args, requirement, revision):
+        cs = _Consistency(requirement, 0, revision)
+        n = C.c_size_t(0)
+        cap = 1024
+        while True:
+            ids = np.zeros(cap, dtype=np.uint32)
+            perms = np.zeros(cap, dtype=np.uint8)
+            rc = fn(self._h, C.byref(cs), *args, ids.ctypes.data, perms.ctypes.data, cap, C.byref(n))
+            if rc == GCK_E_CAPACITY and n.value > cap:
+                cap = n.value  # the engine kept the result: the retry copies it out
+                continue
+            _check(rc)
+            return ids[: n.value], perms[: n.value]
+
+    def lookup_resources(self, resource_type: int, permission: int, subject_type: int, subject_relation: int,
+                         subject_id: int, requirement: int = CONSISTENCY_MIN_LATENCY, revision: int = 0,
+                         now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+        """Ids (ascending) of the resource_type objects the subject has `permission` on, and
+        their permissionship (PERM_HAS / PERM_CONDITIONAL)."""
+        return self._lookup(self._lib.gck_lookup_resources,
+                            (resource_type, permission, subject_type, subject_relation, subject_id, now_us),
+                            requirement, revision)
+
+    def lookup_subjects(self, resource_type: int, resource_id: int, permission: int, subject_type: int,
+                        subject_relation: int = ELLIPSIS, requirement: int = CONSISTENCY_MIN_LATENCY,
+                        revision: int = 0, now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+        """Ids (ascending) of the subject_type subjects that have `permission` on the resource."""
+        return self._lookup(self._lib.gck_lookup_subjects,
+                            (resource_type, resource_id, permission, subject_type, subject_relation, now_us),
+                            requirement, revision)
 
     # ---- partitioned graphs (gck_part_*; driven by gochugaru_amd.partition) -----------------
     def set_partition(self, rank: int, world: int):

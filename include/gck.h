@@ -274,6 +274,24 @@ int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
 
+/* ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) -------- */
+/* Ids of the `resource_type` objects on which the subject has `permission` — HAS or CONDITIONAL,
+ * out_perm[k] says which — ascending. Every object of the type is checked on the device (the
+ * check path's stages, candidates generated and answers compacted there). *out_n = the number of
+ * ids; when it exceeds `cap` nothing is written and GCK_E_CAPACITY is returned: call again with
+ * cap >= *out_n (the result of the last lookup is kept per thread, so the retry does not sweep
+ * again). Errors: GCK_E_NOT_FOUND (unknown type / permission / subject relation),
+ * GCK_E_INVALID_ARGUMENT (a candidate hit the depth budget), GCK_E_REVISION (consistency). */
+int gck_lookup_resources(gck_engine* e, const gck_consistency* cs, uint16_t resource_type, uint16_t permission,
+                         uint16_t subject_type, uint16_t subject_relation, uint32_t subject_id, int64_t now_us,
+                         uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);
+/* Ids of the `subject_type` objects (with `subject_relation`, GCK_ELLIPSIS for plain objects)
+ * that have `permission` on one resource, ascending; same protocol. Concrete subjects only: a
+ * wildcard grant makes every subject of the type match (SpiceDB reports it as the subject "*"). */
+int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resource_type, uint32_t resource_id,
+                        uint16_t permission, uint16_t subject_type, uint16_t subject_relation, int64_t now_us,
+                        uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);
+
 /* ---- partitioned graphs (graphs above one GPU's 288 GB) ----------------
  * Rank r of `world` keeps the rows of the objects it owns (gck_partition_owner) and checks a
  * global batch together with the other ranks, one BFS level per round:

@@ -105,3 +105,15 @@ def test_cycle_is_max_depth_error():
                      "group:b#member@user:x"], max_depth=50)
     assert ck.check(to_oracle_item(parse_check("group:a#member@user:x"))) == (ref.HAS, 0)
     assert ck.check(to_oracle_item(parse_check("group:a#member@user:y"))) == (0, ref.ITEM_ERR_MAX_DEPTH)
+
+
+def test_lookup_resources_known_answers():
+    """client/client_test.go:107-139: LookupResources as the oracle's checks over every document."""
+    g = load_golden("lookup_resources.json")
+    ck = oracle_for(g["schema"], g["tuples"])
+    docs = sorted({t.split("#")[0].split(":")[1] for t in g["tuples"]})
+    for case in g["cases"]:
+        typ, perm = case["permission"].split("#")
+        stype, sid = case["subject"].split(":")
+        got = [d for d in docs if ck.check(ref.Item(typ, d, perm, stype, sid))[0] == ref.HAS]
+        assert got == case["expected"], case["name"]
