@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/pmc_traffic.sh)")
+    ap.add_argument("--host-steps", type=int, default=10, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--bundle-checks", type=int, default=0)
     ap.add_argument("--bundle-frontier", type=int, default=0)
@@ -170,7 +171,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from gochugaru_amd.engine import Engine
+    from gochugaru_amd.engine import Engine, ITEM_DTYPE
 
     t0 = time.time()
     WL = Workload(args, dev)
@@ -262,6 +263,20 @@ def main():
         items = items[rank * args.batch:(rank + 1) * args.batch].contiguous()
     res = perm.cpu().numpy()
     errs = err.cpu().numpy()
+
+    # ---- PCIe-inclusive rate (host buffers: H2D items + kernels + D2H results), never `value` --
+    host_rate = None
+    if WL.kind == "nested" and not args.partitioned and args.host_steps > 0:
+        h_items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+        eng.check_bulk(h_items)
+        t0 = time.perf_counter()
+        for _ in range(args.host_steps):
+            hp, he = eng.check_bulk(h_items)
+        dt_h = time.perf_counter() - t0
+        host_rate = {"value": round(args.host_steps * args.batch / dt_h, 1), "unit": "checks/s",
+                     "ms_per_step": round(dt_h / args.host_steps * 1e3, 4),
+                     "same_results": bool((hp == res).all() and (he == errs).all()),
+                     "note": "gck_check_bulk with host buffers (pageable numpy): 20-B items H2D, 1+4 B results D2H"}
 
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
     prog = tab = None
@@ -377,6 +392,7 @@ def main():
                        if args.partitioned else f"batch-sharded x{world}, graph replicated",
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
             "roofline": roof, "cpu_baseline": cpu,
+            **({"host_buffers": host_rate} if host_rate else {}),
             "oracle_agreement": agree,
             **({"disagreements": disagree} if disagree else {}),
             "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),
