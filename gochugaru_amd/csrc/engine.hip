@@ -983,6 +983,42 @@ void device_free(Engine& e) {
 
 uint64_t device_bytes(const Engine& e) { return e.dev ? e.dev->bytes : 0; }
 
+// Host copies of the committed snapshot's own CSRs (not the derived indexes, which a load
+// rebuilds): the on-disk snapshot cache (snapfile.cpp) writes these.
+void device_export(Engine& e, std::vector<HostCSR>& out) {
+  if (!e.dev) throw Error(GCK_E_STATE, "no snapshot on the device");
+  HIP_OK(hipSetDevice(e.device));
+  HIP_OK(hipDeviceSynchronize());
+  const DeviceSnapshot& ds = *e.dev;
+  out.clear();
+  out.reserve(ds.base.size());
+  for (size_t k = 0; k < ds.base.size(); ++k) {
+    const BaseCsr& b = ds.base[k];
+    const DevCSR& d = ds.table[k];
+    HostCSR h;
+    h.rel = b.rel;
+    h.stype = b.stype;
+    h.srel = b.srel;
+    h.ext = b.ext;
+    h.n_rows = d.n_rows;
+    h.off.resize((size_t)d.n_rows + 1);
+    HIP_OK(hipMemcpy(h.off.data(), d.off, h.off.size() * 4, hipMemcpyDeviceToHost));
+    const uint64_t ne = h.off.back();
+    if (ne != b.n_edges) throw Error(GCK_E_DEVICE, "engine invariant violated: CSR edge count");
+    h.nbr.resize(ne);
+    if (ne) HIP_OK(hipMemcpy(h.nbr.data(), d.nbr, ne * 4, hipMemcpyDeviceToHost));
+    if (b.ext) {
+      h.cav.resize(ne);
+      h.exp_us.resize(ne);
+      if (ne) {
+        HIP_OK(hipMemcpy(h.cav.data(), d.cav, ne * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(h.exp_us.data(), d.exp_us, ne * 8, hipMemcpyDeviceToHost));
+      }
+    }
+    out.push_back(std::move(h));
+  }
+}
+
 // Membership index of a plain CSR (d.off / d.nbr on the device): sets d.mhash, d.mmask and
 // d.has_wild.
 static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {

@@ -140,6 +140,7 @@ struct Engine {
   bool device_ready = false;
   std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
   std::unique_ptr<Schema> schema;
+  std::string schema_text;  // as loaded (the snapshot cache is keyed by it)
   std::vector<TypeInterner> interner;
   // caveat instances: a caveat name + stored context, deduplicated; [0] = none (gck_api.cpp)
   std::vector<std::pair<std::string, std::string>> caveat_instances;
@@ -171,6 +172,12 @@ struct Engine {
 
 // snapshot.cpp
 void add_tuples_text(Engine& e, const char* text, size_t len);
+// gck_api.cpp: caveat instances (a caveat name + stored context)
+void reset_caveats(Engine& e);
+uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json);
+// snapfile.cpp: the on-disk snapshot cache
+void save_snapshot_file(Engine& e, const std::string& path);
+void load_snapshot_file(Engine& e, const std::string& path);
 std::vector<HostCSR> build_csrs(Engine& e);
 // Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
 void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
@@ -188,6 +195,7 @@ void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
 void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
                        uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
 uint64_t device_bytes(const Engine& e);
+void device_export(Engine& e, std::vector<HostCSR>& out);
 // lookups (lookup.inc): candidates [0, n) of the varying id of `proto` (resource id when
 // vary_res, else subject id); matching ids ascending with their permissionship
 void device_lookup(Engine& e, const gck_item& proto, bool vary_res, uint32_t n_candidates, int64_t now_us,

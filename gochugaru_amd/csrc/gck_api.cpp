@@ -16,7 +16,7 @@ thread_local std::string g_last_error;
 
 Engine::~Engine() { device_free(*this); }
 
-static void reset_caveats(Engine& e) {
+void reset_caveats(Engine& e) {
   e.caveat_instances.assign(1, {"", ""});
   e.caveat_ids.clear();
   e.caveat_expr.assign(1, nullptr);
@@ -82,6 +82,7 @@ static std::vector<uint8_t> caveat_table(Engine& e, const char* const* ctxs, con
 }
 
 void stage_tuple(Engine& e, const gck_tuple& t);
+void stage_tuples(Engine& e, const gck_tuple* t, size_t n);
 
 }  // namespace gck
 
@@ -153,6 +154,7 @@ int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
     auto sc = compile_schema(std::string(text ? text : "", len));
     std::unique_lock<std::shared_mutex> lk(e.mu);
     e.schema = std::move(sc);
+    e.schema_text.assign(text ? text : "", len);
     e.interner.assign(e.schema->types.size(), TypeInterner());
     reset_caveats(e);
     e.staged.clear();
@@ -315,8 +317,7 @@ int gck_add_tuples(gck_engine* ge, const gck_tuple* tuples, size_t n) {
     REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
     REQUIRE(n == 0 || tuples, GCK_E_INVALID_ARGUMENT, "null tuples");
     std::unique_lock<std::shared_mutex> lk(e.mu);
-    e.staged.reserve(e.staged.size() + n);
-    for (size_t i = 0; i < n; ++i) stage_tuple(e, tuples[i]);
+    stage_tuples(e, tuples, n);
   });
 }
 
@@ -381,6 +382,25 @@ int gck_commit_snapshot(gck_engine* ge) {
     e.staging = false;
     e.revision = e.staged_revision;
     e.committed = true;
+  });
+}
+
+int gck_save_snapshot(gck_engine* ge, const char* path) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(path, GCK_E_INVALID_ARGUMENT, "null path");
+    std::unique_lock<std::shared_mutex> lk(e.mu);  // no Watch batch may move the snapshot meanwhile
+    save_snapshot_file(e, path);
+  });
+}
+
+int gck_load_snapshot_file(gck_engine* ge, const char* path) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(path, GCK_E_INVALID_ARGUMENT, "null path");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    load_snapshot_file(e, path);
   });
 }
 

@@ -7,6 +7,7 @@
 // expiry times), sorts every row ascending (wildcard id 0xFFFFFFFF sorts last) and keeps the
 // last write of a duplicate relationship (TOUCH semantics).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <numeric>
 #include <thread>
@@ -148,6 +149,53 @@ void stage_tuple(Engine& e, const gck_tuple& t) {
   s.exp_us = t.expires_at_us;
   s.seq = e.seq++;
   e.staged.push_back(s);
+}
+
+// A page of interned tuples (an ExportRelationships page, client/client.go:472-499): validated
+// and staged by up to 16 threads; on an invalid tuple nothing of the page is staged and the
+// error of the first invalid tuple is raised.
+void stage_tuples(Engine& e, const gck_tuple* t, size_t n) {
+  const size_t base = e.staged.size();
+  e.staged.resize(base + n);
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t chunk = std::max<size_t>(1 << 16, (n + hw - 1) / hw);
+  const size_t n_chunks = (n + chunk - 1) / chunk;
+  std::vector<std::string> err(n_chunks);
+  std::vector<int> code(n_chunks, 0);
+  auto work = [&](size_t c) {
+    const size_t lo = c * chunk, hi = std::min(n, lo + chunk);
+    try {
+      for (size_t i = lo; i < hi; ++i) {
+        validate_tuple(e, t[i]);
+        StagedTuple& s = e.staged[base + i];
+        s = StagedTuple{};
+        s.rel = t[i].relation;
+        s.stype = t[i].subject_type;
+        s.srel = t[i].subject_relation;
+        s.obj = t[i].resource_id;
+        s.sid = t[i].subject_id;
+        s.cav = t[i].caveat;
+        s.exp_us = t[i].expires_at_us;
+        s.seq = e.seq + i;
+      }
+    } catch (const Error& x) {
+      code[c] = x.code;
+      err[c] = x.what();
+    }
+  };
+  if (n_chunks <= 1) {
+    if (n) work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (size_t c = 0; c < n_chunks; ++c) pool.emplace_back(work, c);
+    for (std::thread& th : pool) th.join();
+  }
+  for (size_t c = 0; c < n_chunks; ++c)
+    if (code[c]) {
+      e.staged.resize(base);
+      throw Error(code[c], err[c]);
+    }
+  e.seq += n;
 }
 
 namespace {
@@ -330,17 +378,84 @@ std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>&
   return out;
 }
 
+// Orders the staged tuples by (relation, subject type, subject relation, object, subject) with
+// equal relationships in arrival order — the order a comparison sort on (..., seq) gives — by
+// a stable counting sort into (relation, subject kind) groups followed, per group, by a stable
+// LSD radix sort of the 64-bit (object << 32 | subject) keys in 16-bit digits (digits constant
+// over the group are skipped). Groups sort in parallel. Staged tuples are in arrival order.
+static void sort_staged(std::vector<StagedTuple>& v) {
+  const size_t n = v.size();
+  if (n < 2) return;
+  auto gkey = [](const StagedTuple& t) {
+    return ((uint64_t)t.rel << 32) | ((uint64_t)t.stype << 16) | t.srel;
+  };
+  std::vector<uint64_t> gkeys;
+  for (const StagedTuple& t : v) {
+    const uint64_t k = gkey(t);
+    if (gkeys.empty() || gkeys.back() != k) gkeys.push_back(k);
+  }
+  std::sort(gkeys.begin(), gkeys.end());
+  gkeys.erase(std::unique(gkeys.begin(), gkeys.end()), gkeys.end());
+  auto group_of = [&](const StagedTuple& t) {
+    return (size_t)(std::lower_bound(gkeys.begin(), gkeys.end(), gkey(t)) - gkeys.begin());
+  };
+  const size_t G = gkeys.size();
+  std::vector<size_t> start(G + 1, 0);
+  std::vector<uint32_t> g_of(n);
+  for (size_t i = 0; i < n; ++i) {
+    g_of[i] = (uint32_t)group_of(v[i]);
+    ++start[g_of[i] + 1];
+  }
+  for (size_t g = 0; g < G; ++g) start[g + 1] += start[g];
+  std::vector<StagedTuple> out(n);
+  {
+    std::vector<size_t> pos(start.begin(), start.end() - 1);
+    for (size_t i = 0; i < n; ++i) out[pos[g_of[i]]++] = v[i];
+  }
+  std::vector<uint32_t>().swap(g_of);
+  auto sort_group = [&](size_t g) {
+    const size_t b = start[g], m = start[g + 1] - b;
+    if (m < 2) return;
+    struct KI {
+      uint64_t k;
+      uint64_t i;
+    };
+    std::vector<KI> a(m), t(m);
+    uint64_t orv = 0, andv = ~0ull;
+    for (size_t i = 0; i < m; ++i) {
+      const StagedTuple& x = out[b + i];
+      a[i] = {((uint64_t)x.obj << 32) | x.sid, i};
+      orv |= a[i].k;
+      andv &= a[i].k;
+    }
+    std::vector<size_t> cnt(65537);
+    for (int d = 0; d < 4; ++d) {
+      const int sh = 16 * d;
+      if ((((orv ^ andv) >> sh) & 0xFFFF) == 0) continue;  // constant digit
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (size_t i = 0; i < m; ++i) ++cnt[((a[i].k >> sh) & 0xFFFF) + 1];
+      for (size_t j = 0; j < 65536; ++j) cnt[j + 1] += cnt[j];
+      for (size_t i = 0; i < m; ++i) t[cnt[(a[i].k >> sh) & 0xFFFF]++] = a[i];
+      a.swap(t);
+    }
+    for (size_t i = 0; i < m; ++i) v[b + i] = out[b + a[i].i];
+  };
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> pool;
+  std::atomic<size_t> next{0};
+  for (unsigned k = 0; k < std::min<size_t>(hw, G); ++k)
+    pool.emplace_back([&] {
+      for (size_t g; (g = next.fetch_add(1)) < G;) sort_group(g);
+    });
+  for (std::thread& th : pool) th.join();
+  for (size_t g = 0; g < G; ++g)  // groups of one tuple were not copied back
+    if (start[g + 1] - start[g] == 1) v[start[g]] = out[start[g]];
+}
+
 std::vector<HostCSR> build_csrs(Engine& e) {
   const Schema& sc = *e.schema;
   std::vector<StagedTuple>& v = e.staged;
-  std::sort(v.begin(), v.end(), [](const StagedTuple& a, const StagedTuple& b) {
-    if (a.rel != b.rel) return a.rel < b.rel;
-    if (a.stype != b.stype) return a.stype < b.stype;
-    if (a.srel != b.srel) return a.srel < b.srel;
-    if (a.obj != b.obj) return a.obj < b.obj;
-    if (a.sid != b.sid) return a.sid < b.sid;
-    return a.seq < b.seq;
-  });
+  sort_staged(v);
   // keep the last write per (rel, stype, srel, obj, sid)
   size_t w = 0;
   for (size_t i = 0; i < v.size(); ++i) {

@@ -144,6 +144,8 @@ _SIGS = {
     "gck_load_csr": (C.c_int, [_P, C.c_uint16, C.c_uint16, C.c_uint16, C.c_uint32, _P, _P,
                                C.c_uint64, C.c_uint32]),
     "gck_commit_snapshot": (C.c_int, [_P]),
+    "gck_save_snapshot": (C.c_int, [_P, C.c_char_p]),
+    "gck_load_snapshot_file": (C.c_int, [_P, C.c_char_p]),
     "gck_revision": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_tuple_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_device_bytes": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
@@ -362,6 +364,14 @@ class Engine:
 
     def commit_snapshot(self):
         _check(self._lib.gck_commit_snapshot(self._h))
+
+    def save_snapshot(self, path: str):
+        """Writes the committed snapshot to `path` (the on-disk snapshot cache, gck_save_snapshot)."""
+        _check(self._lib.gck_save_snapshot(self._h, os.fsencode(path)))
+
+    def load_snapshot_file(self, path: str):
+        """Replaces the committed snapshot with one saved under the same schema text."""
+        _check(self._lib.gck_load_snapshot_file(self._h, os.fsencode(path)))
 
     def load_snapshot_text(self, revision: int, text: str):
         self.begin_snapshot(revision)

@@ -13,6 +13,7 @@
  *   gck_load_schema
  *       consumes the schema text returned by Client.ReadSchema (client/client.go:416-422).
  *   gck_begin_snapshot / gck_add_tuples / gck_add_tuples_text / gck_load_csr / gck_commit_snapshot
+ *   gck_save_snapshot / gck_load_snapshot_file (on-disk snapshot cache)
  *       consume the relationships streamed by Client.ExportRelationships at the schema's
  *       revision (client/client.go:472-499, rel.FromV1Proto rel/relationship.go:147-172).
  *   gck_intern
@@ -227,6 +228,14 @@ int gck_load_csr(gck_engine* e, uint16_t relation, uint16_t subject_type,
                  uint16_t subject_relation, uint32_t n_rows, const uint32_t* offsets,
                  const uint32_t* neighbours, uint64_t n_edges, uint32_t mem_flags);
 int gck_commit_snapshot(gck_engine* e);
+/* On-disk snapshot cache, in place of re-reading the snapshot through
+ * Client.ExportRelationships (client/client.go:472-499) and re-interning it: save writes the
+ * committed snapshot (interner, caveat instances, base CSRs, revision) keyed by the schema
+ * text; load (same schema text, no staging in progress) replaces the committed snapshot and
+ * rebuilds the derived device indexes. GCK_E_SCHEMA when the file was saved under another
+ * schema; GCK_E_STATE to save a partitioned engine or with nothing committed. */
+int gck_save_snapshot(gck_engine* e, const char* path);
+int gck_load_snapshot_file(gck_engine* e, const char* path);
 int gck_revision(gck_engine* e, uint64_t* out);
 int gck_tuple_count(gck_engine* e, uint64_t* out);
 /* Bytes resident in HBM for the snapshot (CSR + tables). */

@@ -9,3 +9,4 @@ GCK_DEBUG_TIMING=$OUT/t timeout -k 10 300 python bench.py --steps 3 --warmup 1 -
 python tests/analyze_timing.py "$OUT/t.bin" > "$OUT/t.txt"
 cat "$OUT/t.txt"
 touch gochugaru_amd/csrc/bundle.inc && make -C gochugaru_amd/csrc > /dev/null
+rm -f "$OUT/t.bin"
