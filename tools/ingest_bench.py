@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tuples", type=float, default=1e8)
     ap.add_argument("--file", default="/tmp/gck_ingest_bench.gck")
+    ap.add_argument("--file-only", action="store_true", help="only the snapshot file (save from the prebuilt engine)")
     args = ap.parse_args()
     import torch
     from gochugaru_amd.engine import ELLIPSIS, TUPLE_DTYPE, Engine
@@ -31,6 +32,29 @@ def main():
     items = synth.checks(G, 65536, seed=31)
     ref = load_engine(G)
     p0, e0 = run(ref, items)
+    if args.file_only:
+        t0 = time.perf_counter()
+        ref.save_snapshot(args.file)
+        t_save = time.perf_counter() - t0
+        n = int(ref.tuple_count)
+        ref.close()
+        f = Engine(device=0)
+        f.load_schema(synth.SCHEMA)
+        t0 = time.perf_counter()
+        f.load_snapshot_file(args.file)
+        torch.cuda.synchronize()
+        t_load = time.perf_counter() - t0
+        p2, e2 = run(f, items)
+        f.close()
+        size = os.path.getsize(args.file)
+        os.remove(args.file)
+        same = bool((p0 == p2).all() and (e0 == e2).all())
+        print(json.dumps({"workload": "config4-deep-nested-groups", "tuples": n,
+                          "snapshot_file": {"bytes": size, "save_s": round(t_save, 2), "load_s": round(t_load, 2),
+                                            "load_tuples_per_s": round(n / t_load)},
+                          "same_results_64k": same}))
+        assert same
+        return
     ref.close()
 
     H = synth.host_arrays(G)
