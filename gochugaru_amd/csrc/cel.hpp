@@ -19,7 +19,9 @@ namespace gck {
 namespace cel {
 
 struct Value {
-  enum Kind : uint8_t { UNKNOWN, NUL, BOOL, INT, DBL, STR, LIST, MAP } k = UNKNOWN;
+  // TS (timestamp) and DUR (duration) hold microseconds in `i`; IP holds the 4 or 16 address
+  // bytes in `s`
+  enum Kind : uint8_t { UNKNOWN, NUL, BOOL, INT, DBL, STR, LIST, MAP, TS, DUR, IP } k = UNKNOWN;
   bool b = false;
   int64_t i = 0;
   double d = 0;
@@ -37,8 +39,11 @@ Object parse_context(const std::string& json);
 struct Node;
 
 // Compiles a caveat body (the CEL text between the braces of `caveat name(...) { ... }`).
-// Throws Error(GCK_E_SCHEMA).
-std::shared_ptr<const Node> compile(const std::string& body);
+// `params` (name, declared type): a parameter declared timestamp / duration / ipaddress takes
+// its context value as text (RFC 3339, Go duration syntax, an IPv4/IPv6 address) and is
+// converted on lookup. Throws Error(GCK_E_SCHEMA).
+std::shared_ptr<const Node> compile(const std::string& body,
+                                    const std::vector<std::pair<std::string, std::string>>& params = {});
 
 enum Outcome : uint8_t { FALSE = 0, TRUE = 1, PARTIAL = 2 };
 

@@ -284,7 +284,7 @@ class Parser {
       body += t.v;
     }
     c.body = body;
-    c.expr = cel::compile(body);
+    c.expr = cel::compile(body, c.params);
     if (sc.caveats.count(c.name)) fail("duplicate caveat '" + c.name + "'");
     sc.caveats[c.name] = std::move(c);
   }

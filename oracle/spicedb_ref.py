@@ -38,6 +38,7 @@ subtracted Y -> N, else ERR, else C, else Y.
 """
 from __future__ import annotations
 
+import datetime
 import re
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
@@ -308,7 +309,7 @@ class Schema:
                 depth -= 1
         body = self._toks[start : self._i - 1]
         c = Caveat(name, params, " ".join(v for _, v in body))
-        c.expr = CelParser(body).parse()
+        c.expr = CelParser(body, params).parse()
         self.caveats[name] = c
 
     def _validate(self):
@@ -364,9 +365,23 @@ class CelParser:
     """Recursive-descent parser for a CEL subset: literals, identifiers, member access on
     maps, lists, ! - unary, * / %, + -, comparisons, in, &&, ||, ?:."""
 
-    def __init__(self, toks):
+    def __init__(self, toks, params=None):
         self.t = list(toks) + [("eof", "")]
         self.i = 0
+        self.conv = {k: v for k, v in (params or {}).items() if v in ("timestamp", "duration", "ipaddress")}
+
+    def args(self):
+        out = []
+        while self.peek() != ("op", ")"):
+            if self.peek()[0] == "eof":
+                raise SchemaError("unterminated argument list")
+            out.append(self.ternary())
+            if self.peek() == ("op", ","):
+                self.nxt()
+            elif self.peek() != ("op", ")"):
+                raise SchemaError("expected ',' or ')'")
+        self.nxt()
+        return out
 
     def peek(self):
         return self.t[self.i]
@@ -442,7 +457,12 @@ class CelParser:
         while True:
             if self.peek() == ("op", "."):
                 self.nxt()
-                e = (".", e, self.nxt()[1])
+                f = self.nxt()[1]
+                if self.peek() == ("op", "("):  # method call
+                    self.nxt()
+                    e = ("call", f, True, [e] + self.args())
+                else:
+                    e = (".", e, f)
             elif self.peek() == ("op", "["):
                 self.nxt()
                 k = self.ternary()
@@ -457,7 +477,7 @@ class CelParser:
         if kind == "num":
             return ("lit", float(v) if "." in v else int(v))
         if kind == "str":
-            return ("lit", bytes(v[1:-1], "utf-8").decode("unicode_escape"))
+            return ("lit", _unescape(v[1:-1]))
         if kind == "ident":
             if v == "true":
                 return ("lit", True)
@@ -465,7 +485,15 @@ class CelParser:
                 return ("lit", False)
             if v == "null":
                 return ("lit", None)
-            return ("var", v)
+            if self.peek() == ("op", "("):  # global function, or the has() macro
+                self.nxt()
+                a = self.args()
+                if v == "has":
+                    if len(a) != 1 or a[0][0] != ".":
+                        raise SchemaError("has() takes one field selection")
+                    return ("has", a[0][1], a[0][2])
+                return ("call", v, False, a)
+            return ("var", v, self.conv.get(v))
         if (kind, v) == ("op", "("):
             e = self.ternary()
             if self.nxt() != ("op", ")"):
@@ -482,6 +510,21 @@ class CelParser:
         raise SchemaError(f"unexpected token {v!r} in caveat expression")
 
 
+_ESCAPES = {"n": "\n", "t": "\t", "r": "\r", "\\": "\\", "'": "'", '"': '"'}
+_ESCAPE_RE = re.compile(r"\\(x[0-9A-Fa-f]{2}|u[0-9A-Fa-f]{4}|.)", re.DOTALL)
+
+
+def _unescape(body: str) -> str:
+    """CEL string literal body: the common escapes, \\xHH and \\uXXXX as code points; other
+    characters (non-ASCII included) stand for themselves."""
+    def sub(m):
+        t = m.group(1)
+        if t[0] in "xu" and len(t) > 1:
+            return chr(int(t[1:], 16))
+        return _ESCAPES.get(t, "\\" + t)
+    return _ESCAPE_RE.sub(sub, body)
+
+
 def cel_eval(e, env: Dict[str, Any]):
     """Evaluate with partial knowledge: returns a value, or UNKNOWN if the result depends on
     a missing parameter (SpiceDB returns CONDITIONAL_PERMISSION in that case)."""
@@ -489,7 +532,22 @@ def cel_eval(e, env: Dict[str, Any]):
     if op == "lit":
         return e[1]
     if op == "var":
-        return env.get(e[1], UNKNOWN)
+        v = env.get(e[1], UNKNOWN)
+        conv = e[2] if len(e) > 2 else None
+        if conv is None or v is UNKNOWN or isinstance(v, _CONV_TYPE[conv]):
+            return v
+        if not isinstance(v, str):
+            raise ValueError(f"parameter {e[1]!r} has the wrong type")
+        return _CONV_FN[conv](v)
+    if op == "has":
+        a = cel_eval(e[1], env)
+        if a is UNKNOWN:
+            return UNKNOWN
+        if not isinstance(a, dict):
+            raise ValueError("has() on a non-map")
+        return e[2] in a
+    if op == "call":
+        return _cel_call(e, env)
     if op == "list":
         vals = [cel_eval(x, env) for x in e[1]]
         return UNKNOWN if any(v is UNKNOWN for v in vals) else vals
@@ -543,6 +601,8 @@ def cel_eval(e, env: Dict[str, Any]):
         return a >= b
     if op == "in":
         return a in b
+    if isinstance(a, (Timestamp, Duration, IPAddress)) or isinstance(b, (Timestamp, Duration, IPAddress)):
+        return _cel_temporal(op, a, b)
     if op == "+":
         return a + b
     if op == "-":
@@ -554,6 +614,222 @@ def cel_eval(e, env: Dict[str, Any]):
     if op == "%":
         return a % b
     raise SchemaError(f"unsupported CEL operator {op!r}")
+
+
+# -- CEL standard functions over timestamps, durations and strings, and SpiceDB's ipaddress ---
+# (SURVEY §8 f4). Timestamps and durations are whole microseconds (RFC 3339 fractions and Go
+# duration components below 1 us are truncated); accessors are UTC.
+
+@dataclass(frozen=True, order=True)
+class Timestamp:
+    us: int
+
+
+@dataclass(frozen=True, order=True)
+class Duration:
+    us: int
+
+
+@dataclass(frozen=True)
+class IPAddress:
+    packed: bytes
+
+
+_RFC3339 = re.compile(r"^(\d{4})-(\d{2})-(\d{2})[Tt](\d{2}):(\d{2}):(\d{2})(?:\.(\d+))?(?:([Zz])|([+-])(\d{2}):(\d{2}))$")
+
+
+def parse_timestamp(s: str) -> Timestamp:
+    m = _RFC3339.match(s)
+    if not m:
+        raise ValueError(f"not an RFC 3339 timestamp: {s!r}")
+    y, mo, d, h, mi, se = (int(m.group(k)) for k in range(1, 7))
+    if h > 23 or mi > 59 or se > 59:
+        raise ValueError(f"not an RFC 3339 timestamp: {s!r}")
+    day = datetime.date(y, mo, d)  # ValueError on an impossible date
+    frac = int((m.group(7) or "")[:6].ljust(6, "0"))
+    off = 0
+    if m.group(9):
+        oh, om = int(m.group(10)), int(m.group(11))
+        if oh > 23 or om > 59:
+            raise ValueError(f"not an RFC 3339 timestamp: {s!r}")
+        off = (1 if m.group(9) == "+" else -1) * (oh * 3600 + om * 60)
+    days = (day - datetime.date(1970, 1, 1)).days
+    return Timestamp(((days * 86400 + h * 3600 + mi * 60 + se) - off) * 1_000_000 + frac)
+
+
+_DUR_UNITS = {"ns": 1, "us": 1000, "\u00b5s": 1000, "ms": 1_000_000, "s": 1_000_000_000, "m": 60_000_000_000,
+              "h": 3_600_000_000_000}
+_DUR_PART = re.compile(r"(\d*)(?:\.(\d*))?(ns|us|\u00b5s|ms|s|m|h)")
+
+
+def parse_duration(s: str) -> Duration:
+    t, neg = s, False
+    if t[:1] in ("-", "+"):
+        neg, t = t[0] == "-", t[1:]
+    if t == "0":
+        return Duration(0)
+    if not t:
+        raise ValueError(f"not a duration: {s!r}")
+    ns, pos = 0, 0
+    while pos < len(t):
+        m = _DUR_PART.match(t, pos)
+        if not m or (not m.group(1) and not m.group(2)):
+            raise ValueError(f"not a duration: {s!r}")
+        unit = _DUR_UNITS[m.group(3)]
+        frac = (m.group(2) or "")[:18]
+        ns += int(m.group(1) or "0") * unit + (int(frac) * unit // 10 ** len(frac) if frac else 0)
+        pos = m.end()
+    us = ns // 1000
+    if us > (2 ** 63 - 1) // 2:
+        raise ValueError(f"duration out of range: {s!r}")
+    return Duration(-us if neg else us)
+
+
+def parse_ipaddress(s: str) -> IPAddress:
+    import ipaddress
+    if ":" not in s:
+        parts = s.split(".")
+        if len(parts) != 4 or any(not p.isdigit() or not p.isascii() or len(p) > 3 or (len(p) > 1 and p[0] == "0")
+                                  or int(p) > 255 for p in parts):
+            raise ValueError(f"not an IP address: {s!r}")
+    return IPAddress(ipaddress.ip_address(s).packed)
+
+
+def _in_cidr(ip: IPAddress, cidr: str) -> bool:
+    net, _, bits = cidr.partition("/")
+    if not bits or not bits.isdigit() or not bits.isascii() or len(bits) > 3:
+        raise ValueError(f"invalid CIDR {cidr!r}")
+    n = int(bits)
+    base = parse_ipaddress(net).packed
+    if n > len(base) * 8:
+        raise ValueError(f"invalid CIDR {cidr!r}")
+    if len(ip.packed) != len(base):
+        return False
+    a, b = int.from_bytes(ip.packed, "big"), int.from_bytes(base, "big")
+    shift = len(base) * 8 - n
+    return (a >> shift) == (b >> shift)
+
+
+_CONV_TYPE = {"timestamp": Timestamp, "duration": Duration, "ipaddress": IPAddress}
+_CONV_FN = {"timestamp": parse_timestamp, "duration": parse_duration, "ipaddress": parse_ipaddress}
+
+
+def _trunc_div(a: int, b: int) -> int:
+    q = abs(a) // b
+    return -q if a < 0 else q
+
+
+def _cel_temporal(op, a, b):
+    if op == "+":
+        if isinstance(a, Duration) and isinstance(b, Duration):
+            return Duration(a.us + b.us)
+        if isinstance(a, Timestamp) and isinstance(b, Duration):
+            return Timestamp(a.us + b.us)
+        if isinstance(a, Duration) and isinstance(b, Timestamp):
+            return Timestamp(a.us + b.us)
+    if op == "-":
+        if isinstance(a, Timestamp) and isinstance(b, Timestamp):
+            return Duration(a.us - b.us)
+        if isinstance(a, Timestamp) and isinstance(b, Duration):
+            return Timestamp(a.us - b.us)
+        if isinstance(a, Duration) and isinstance(b, Duration):
+            return Duration(a.us - b.us)
+    if op in ("<", "<=", ">", ">=") and type(a) is type(b) and not isinstance(a, IPAddress):
+        return {"<": a.us < b.us, "<=": a.us <= b.us, ">": a.us > b.us, ">=": a.us >= b.us}[op]
+    if op == "in" and isinstance(b, list):
+        return any(a == x for x in b)
+    raise ValueError(f"{op!r} on incompatible values")
+
+
+def _cel_call(e, env):
+    _, f, method, kids = e
+    a = []
+    for k in kids:
+        v = cel_eval(k, env)
+        if v is UNKNOWN:
+            return UNKNOWN
+        a.append(v)
+
+    def want(n):
+        if len(a) != n:
+            raise ValueError(f"{f}(): wrong number of arguments")
+
+    if f == "size":
+        want(1)
+        if isinstance(a[0], (str, list, dict)) and not isinstance(a[0], bool):
+            return len(a[0])
+        raise ValueError("size() of a value without a size")
+    if method and f in ("startsWith", "endsWith", "contains"):
+        want(2)
+        if not isinstance(a[0], str) or not isinstance(a[1], str):
+            raise ValueError(f"{f}() needs strings")
+        return {"startsWith": a[0].startswith, "endsWith": a[0].endswith,
+                "contains": a[0].__contains__}[f](a[1])
+    if not method and f in ("timestamp", "duration", "ipaddress"):
+        want(1)
+        if isinstance(a[0], _CONV_TYPE[f]):
+            return a[0]
+        if not isinstance(a[0], str):
+            raise ValueError(f"{f}(): needs a string")
+        return _CONV_FN[f](a[0])
+    if method and f == "in_cidr":
+        want(2)
+        if not isinstance(a[0], IPAddress) or not isinstance(a[1], str):
+            raise ValueError("in_cidr() needs an ipaddress and a string")
+        return _in_cidr(a[0], a[1])
+    if not method and f == "int":
+        want(1)
+        x = a[0]
+        if isinstance(x, bool):
+            raise ValueError("int(): unsupported argument")
+        if isinstance(x, int):
+            return x
+        if isinstance(x, float):
+            if not (-9.2e18 < x < 9.2e18):
+                raise ValueError("int(): out of range")
+            return int(x)
+        if isinstance(x, str):
+            body = x[1:] if x[:1] in ("-", "+") else x
+            if not body or len(body) > 18 or not (body.isdigit() and body.isascii()):
+                raise ValueError("int(): not an integer string")
+            return int(x)
+        if isinstance(x, Timestamp):
+            return x.us // 1_000_000
+        raise ValueError("int(): unsupported argument")
+    if not method and f == "double":
+        want(1)
+        x = a[0]
+        if isinstance(x, float):
+            return x
+        if isinstance(x, int) and not isinstance(x, bool):
+            return float(x)
+        raise ValueError("double(): unsupported argument")
+    if not method and f == "string":
+        want(1)
+        x = a[0]
+        if isinstance(x, str):
+            return x
+        if isinstance(x, bool):
+            return "true" if x else "false"
+        if isinstance(x, int):
+            return str(x)
+        raise ValueError("string(): unsupported argument")
+    if method and len(a) == 1 and isinstance(a[0], Timestamp):
+        secs = a[0].us // 1_000_000
+        days, sod = secs // 86400, secs % 86400
+        day = datetime.date(1970, 1, 1) + datetime.timedelta(days=days)
+        acc = {"getFullYear": day.year, "getMonth": day.month - 1, "getDate": day.day,
+               "getDayOfMonth": day.day - 1, "getDayOfWeek": (day.weekday() + 1) % 7,
+               "getDayOfYear": day.timetuple().tm_yday - 1, "getHours": sod // 3600,
+               "getMinutes": sod // 60 % 60, "getSeconds": sod % 60,
+               "getMilliseconds": (a[0].us - secs * 1_000_000) // 1000}
+        if f in acc:
+            return acc[f]
+    if method and len(a) == 1 and isinstance(a[0], Duration):
+        per = {"getHours": 3_600_000_000, "getMinutes": 60_000_000, "getSeconds": 1_000_000, "getMilliseconds": 1000}
+        if f in per:
+            return _trunc_div(a[0].us, per[f])
+    raise ValueError(f"unknown function {f!r}")
 
 
 # ----------------------------------------------------------------------------------------

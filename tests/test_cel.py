@@ -210,3 +210,159 @@ def test_caveat_instances_deduplicate(eng):
     assert a == b and a != c and a > 0
     with pytest.raises(E.GckError):
         eng.add_caveat_instance("only_on_tuesday", '{"day_of_the_week":')
+
+
+# ---- CEL standard functions, timestamps, durations, ipaddress --------------
+# Known answers derived by hand (calendar facts, CIDR arithmetic); the oracle must agree with
+# them and the engine with both. Parity with SpiceDB itself is unpinned.
+F4_SCHEMA = """caveat f(now timestamp, t2 timestamp, win duration, ip ipaddress, s string, n int, m map<any>, l list<int>) { EXPR }
+definition user {}"""
+F4_CTX = {"now": "2025-10-03T12:34:56.789Z", "t2": "2024-02-29T23:00:00-01:00", "win": "1h30m",
+          "ip": "10.1.2.3", "s": "héllo", "n": 7, "m": {"k": 1}, "l": [1, 2, 3]}
+F4_CASES = [
+    ("now.getFullYear() == 2025 && now.getMonth() == 9 && now.getDate() == 3", True),
+    ("now.getDayOfMonth() == 2 && now.getDayOfWeek() == 5", True),  # 2025-10-03 was a Friday
+    ("now.getDayOfYear() == 275", True),  # 31+28+31+30+31+30+31+31+30 = 273 days, then day 3 -> index 275
+    ("now.getHours() == 12 && now.getMinutes() == 34 && now.getSeconds() == 56 && now.getMilliseconds() == 789", True),
+    ("t2.getMonth() == 2 && t2.getDate() == 1 && t2.getHours() == 0", True),  # 23:00 at -01:00 = 00:00Z next day
+    ("t2 == timestamp(\"2024-03-01T00:00:00Z\")", True),
+    ("now - t2 > duration(\"13000h\") && now - t2 < duration(\"14000h\")", True),
+    ("t2 + duration(\"24h\") == timestamp(\"2024-03-02T00:00:00Z\")", True),
+    ("now > t2 && t2 < now && !(now < t2)", True),
+    ("win == duration(\"90m\") && win.getMinutes() == 90 && win.getHours() == 1", True),
+    ("duration(\"1.5s\").getMilliseconds() == 1500 && duration(\"-1.5h\").getMinutes() == -90", True),
+    ("duration(\"300ms\") + duration(\"700ms\") == duration(\"1s\")", True),
+    ("duration(\"1h\") - duration(\"61m\") < duration(\"0\")", True),
+    ("int(timestamp(\"1970-01-01T00:00:10Z\")) == 10 && int(timestamp(\"1969-12-31T23:59:59.5Z\")) == -1", True),
+    ("ip.in_cidr(\"10.0.0.0/8\") && !ip.in_cidr(\"10.2.0.0/16\") && ip.in_cidr(\"10.1.2.3/32\")", True),
+    ("ipaddress(\"2001:db8::1\").in_cidr(\"2001:db8::/32\") && !ipaddress(\"2001:db8::1\").in_cidr(\"10.0.0.0/8\")", True),
+    ("ip == ipaddress(\"10.1.2.3\") && ip != ipaddress(\"10.1.2.4\")", True),
+    ("size(s) == 5 && s.size() == 5 && s.startsWith(\"hé\") && s.endsWith(\"llo\") && s.contains(\"él\")", True),
+    ("size(l) == 3 && size(m) == 1 && has(m.k) && !has(m.z)", True),
+    ("int(\"-42\") == -42 && int(3.9) == 3 && int(-3.9) == -3 && double(n) == 7.0", True),
+    ("string(n) == \"7\" && string(true) == \"true\" && string(\"x\") == \"x\"", True),
+    ("now.getDayOfWeek() == 1", False),
+]
+F4_ERRORS = ["timestamp(\"2025-02-30T00:00:00Z\") == now", "duration(\"5 days\") == win", "int(\"1.5\") == 1",
+             "ipaddress(\"10.0.0.256\") == ip", "ip.in_cidr(\"10.0.0.0/33\")", "size(n) == 1", "s.startsWith(n)",
+             "now < win", "now + now == now", "nosuch(1) == 1"]
+
+
+def _f4(expr):
+    return F4_SCHEMA.replace("EXPR", expr)
+
+
+@pytest.mark.parametrize("expr,want", F4_CASES)
+def test_f4_known_answers(eng, expr, want):
+    schema = _f4(expr)
+    eng.load_schema(schema)
+    expected = E.CAVEAT_TRUE if want else E.CAVEAT_FALSE
+    assert oracle_outcome(ref.Schema(schema).caveats["f"].expr, None, F4_CTX) == expected
+    assert engine_outcome(eng, "f", None, F4_CTX) == expected
+    # the same with every parameter missing: unknown unless the expression needs none of them
+    assert engine_outcome(eng, "f", None, {}) == oracle_outcome(ref.Schema(schema).caveats["f"].expr, None, {})
+
+
+@pytest.mark.parametrize("expr", F4_ERRORS)
+def test_f4_errors(eng, expr):
+    schema = _f4(expr)
+    eng.load_schema(schema)
+    assert oracle_outcome(ref.Schema(schema).caveats["f"].expr, None, F4_CTX) == "error"
+    assert engine_outcome(eng, "f", None, F4_CTX) == "error"
+
+
+def test_f4_typed_parameters(eng):
+    """Declared timestamp / duration / ipaddress parameters take their context value as text;
+    text that does not convert is an evaluation error, a missing parameter stays unknown."""
+    schema = _f4("now > timestamp(\"2025-01-01T00:00:00Z\") && win < duration(\"2h\") && ip.in_cidr(\"10.0.0.0/8\")")
+    eng.load_schema(schema)
+    expr = ref.Schema(schema).caveats["f"].expr
+    for ctx, want in (({**F4_CTX}, E.CAVEAT_TRUE), ({**F4_CTX, "win": "3h"}, E.CAVEAT_FALSE),
+                      ({**F4_CTX, "now": "yesterday"}, "error"), ({**F4_CTX, "ip": 10}, "error"),
+                      ({"win": "3h"}, E.CAVEAT_FALSE), ({"win": "1h"}, E.CAVEAT_PARTIAL)):
+        assert oracle_outcome(expr, None, ctx) == want, ctx
+        assert engine_outcome(eng, "f", None, ctx) == want, ctx
+
+
+TS_POOL = ["1970-01-01T00:00:00Z", "2025-10-03T00:00:00Z", "2025-10-03T23:59:59.999999Z", "2024-02-29T12:00:00+05:30",
+           "1999-12-31T23:59:59-08:00", "2000-03-01T00:00:00.5Z", "1969-07-20T20:17:40Z", "2038-01-19T03:14:08Z"]
+DUR_POOL = ["0", "1h", "90m", "1.5s", "-2h", "300ms", "1h2m3.5s", "250us", "7ns", "36h", "-0.5m", "1000000s"]
+IP_POOL = ["10.1.2.3", "10.255.0.1", "192.168.1.1", "127.0.0.1", "2001:db8::1", "::1", "fe80::1"]
+CIDR_POOL = ["10.0.0.0/8", "10.1.0.0/16", "192.168.0.0/24", "0.0.0.0/0", "127.0.0.1/32", "2001:db8::/32", "::/0"]
+ACCESSORS = ["getFullYear", "getMonth", "getDate", "getDayOfMonth", "getDayOfWeek", "getDayOfYear", "getHours",
+             "getMinutes", "getSeconds", "getMilliseconds"]
+
+
+def gen_f4(rng, depth):
+    """A random boolean expression over the f4 functions (parameters now/t2 timestamp, win
+    duration, ip ipaddress, s string)."""
+    def ts():
+        return rng.choice(["now", "t2", f'timestamp("{rng.choice(TS_POOL)}")',
+                           f'(now + duration("{rng.choice(DUR_POOL)}"))', f'(t2 - duration("{rng.choice(DUR_POOL)}"))'])
+
+    def dur():
+        return rng.choice(["win", f'duration("{rng.choice(DUR_POOL)}")', f"({ts()} - {ts()})",
+                           f'(win + duration("{rng.choice(DUR_POOL)}"))'])
+
+    def leaf():
+        k = rng.randrange(7)
+        if k == 0:
+            return f"({ts()} {rng.choice(['<', '<=', '>', '>=', '==', '!='])} {ts()})"
+        if k == 1:
+            return f"({dur()} {rng.choice(['<', '<=', '>', '>=', '==', '!='])} {dur()})"
+        if k == 2:
+            return f"({ts()}.{rng.choice(ACCESSORS)}() {rng.choice(['<', '==', '>='])} {rng.randint(0, 60)})"
+        if k == 3:
+            return f"({dur()}.{rng.choice(ACCESSORS[6:])}() {rng.choice(['<', '==', '>='])} {rng.randint(-100, 100)})"
+        if k == 4:
+            ipx = rng.choice(["ip", f'ipaddress("{rng.choice(IP_POOL)}")'])
+            return f'{ipx}.in_cidr("{rng.choice(CIDR_POOL)}")'
+        if k == 5:
+            lit = rng.choice(['"ab"', '"b"', '""', '"é"', '"xyz"'])
+            return f"s.{rng.choice(['startsWith', 'endsWith', 'contains'])}({lit})"
+        return f"(size(s) {rng.choice(['<', '==', '>'])} {rng.randint(0, 4)})"
+
+    if depth == 0:
+        return leaf()
+    op = rng.choice(["&&", "||", "!", "leaf"])
+    if op == "!":
+        return f"!({gen_f4(rng, depth - 1)})"
+    if op == "leaf":
+        return leaf()
+    return f"({gen_f4(rng, depth - 1)} {op} {gen_f4(rng, depth - 1)})"
+
+
+def rand_f4_context(rng):
+    ctx = {}
+    if rng.random() < 0.7:
+        ctx["now"] = rng.choice(TS_POOL + ["2025-13-01T00:00:00Z"] if rng.random() < 0.05 else TS_POOL)
+    if rng.random() < 0.7:
+        ctx["t2"] = rng.choice(TS_POOL)
+    if rng.random() < 0.7:
+        ctx["win"] = rng.choice(DUR_POOL + ["1d"] if rng.random() < 0.05 else DUR_POOL)
+    if rng.random() < 0.7:
+        ctx["ip"] = rng.choice(IP_POOL)
+    if rng.random() < 0.7:
+        ctx["s"] = rng.choice(["abc", "b", "", "é", "xyzab"])
+    return ctx
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_f4_random_expressions_match_oracle(eng, seed):
+    rng = random.Random(7000 + seed)
+    bodies = [gen_f4(rng, rng.randint(0, 3)) for _ in range(40)]
+    params = "now timestamp, t2 timestamp, win duration, ip ipaddress, s string"
+    schema = "".join(f"caveat g{i}({params}) {{ {b} }}\n" for i, b in enumerate(bodies)) + "definition user {}\n"
+    eng.load_schema(schema)
+    sc = ref.Schema(schema)
+    seen = set()
+    for i, body in enumerate(bodies):
+        expr = sc.caveats[f"g{i}"].expr
+        for _ in range(10):
+            stored = rand_f4_context(rng) if rng.random() < 0.4 else None
+            context = rand_f4_context(rng)
+            want = oracle_outcome(expr, stored, context)
+            got = engine_outcome(eng, f"g{i}", stored, context)
+            assert got == want, (body, stored, context)
+            seen.add(want)
+    assert {E.CAVEAT_TRUE, E.CAVEAT_FALSE, E.CAVEAT_PARTIAL} <= seen
