@@ -165,6 +165,7 @@ struct Engine {
   Workspace* ws = nullptr;
   uint64_t generation = 0;        // bumped by every device snapshot (commit, Watch batch)
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
+  void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
   size_t delta_scratch_cap = 0;
   gck_stats stats{};
   ~Engine();
