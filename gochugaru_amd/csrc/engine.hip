@@ -1161,31 +1161,37 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     ds->n_csrs = (uint32_t)table.size();
     ds->n_types = (uint32_t)sc.types.size();
     ds->n_rels = (uint32_t)sc.rels.size();
-    ds->nodes = dalloc<DevNode>(ds->allocs, nodes.size(), &ds->bytes);
-    ds->items = dalloc<DevItem>(ds->allocs, items.size(), &ds->bytes);
-    ds->csrs = dalloc<DevCSR>(ds->allocs, table.size(), &ds->bytes);
-    ds->type_counts = dalloc<uint32_t>(ds->allocs, sc.types.size(), &ds->bytes);
-    HIP_OK(hipMemcpy(ds->nodes, nodes.data(), nodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
-    if (!items.empty())
-      HIP_OK(hipMemcpy(ds->items, items.data(), items.size() * sizeof(DevItem), hipMemcpyHostToDevice));
-    if (!table.empty())
-      HIP_OK(hipMemcpy(ds->csrs, table.data(), table.size() * sizeof(DevCSR), hipMemcpyHostToDevice));
+    // the program tables and the caveat-instance tables in one device block and one upload (a
+    // synchronous copy each would cost a Watch batch ~20 us apiece)
     std::vector<uint32_t> counts(sc.types.size());
     for (size_t t = 0; t < counts.size(); ++t) counts[t] = e.interner[t].count;
-    HIP_OK(hipMemcpy(ds->type_counts, counts.data(), counts.size() * 4, hipMemcpyHostToDevice));
-    // caveat instances: outcome under the stored context, row of the per-batch table
-    {
-      std::vector<uint8_t> st(e.caveat_static);
-      std::vector<uint32_t> row(e.caveat_row);
-      if (st.empty()) {
-        st.push_back(1);
-        row.push_back(kNone);
-      }
-      ds->cav_static = dalloc<uint8_t>(ds->allocs, st.size(), &ds->bytes);
-      ds->cav_row = dalloc<uint32_t>(ds->allocs, row.size(), &ds->bytes);
-      HIP_OK(hipMemcpy(ds->cav_static, st.data(), st.size(), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(ds->cav_row, row.data(), row.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint8_t> cst(e.caveat_static);  // outcome under the stored context
+    std::vector<uint32_t> crow(e.caveat_row);   // row of the per-call outcome table
+    if (cst.empty()) {
+      cst.push_back(1);
+      crow.push_back(kNone);
     }
+    std::vector<unsigned char> blob;
+    auto put = [&](const void* src, size_t n) {
+      const size_t o = (blob.size() + 255) & ~(size_t)255;
+      blob.resize(o + std::max<size_t>(n, 1));
+      if (n) std::memcpy(blob.data() + o, src, n);
+      return o;
+    };
+    const size_t o_nodes = put(nodes.data(), nodes.size() * sizeof(DevNode));
+    const size_t o_items = put(items.data(), items.size() * sizeof(DevItem));
+    const size_t o_csrs = put(table.data(), table.size() * sizeof(DevCSR));
+    const size_t o_counts = put(counts.data(), counts.size() * 4);
+    const size_t o_cst = put(cst.data(), cst.size());
+    const size_t o_crow = put(crow.data(), crow.size() * 4);
+    unsigned char* d_blob = dalloc<unsigned char>(ds->allocs, blob.size(), &ds->bytes);
+    HIP_OK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    ds->nodes = reinterpret_cast<DevNode*>(d_blob + o_nodes);
+    ds->items = reinterpret_cast<DevItem*>(d_blob + o_items);
+    ds->csrs = reinterpret_cast<DevCSR*>(d_blob + o_csrs);
+    ds->type_counts = reinterpret_cast<uint32_t*>(d_blob + o_counts);
+    ds->cav_static = d_blob + o_cst;
+    ds->cav_row = reinterpret_cast<uint32_t*>(d_blob + o_crow);
     ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
     if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
     ds->q_bits = 31 - ds->node_bits;
