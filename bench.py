@@ -314,7 +314,8 @@ def main():
         traffic, traffic_src = None, None
         if args.traffic_json and os.path.exists(args.traffic_json) and WL.kind == "nested":
             tj = json.load(open(args.traffic_json))
-            traffic, traffic_src = tj.get("hbm_bytes_per_batch"), args.traffic_json
+            traffic = tj.get("hbm_bytes_per_batch")
+            traffic_src = os.path.relpath(args.traffic_json, os.path.dirname(os.path.abspath(__file__)))
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "kernel": "k_bundles<1> + k_bundles<16> (one launch each per batch)",
