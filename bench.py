@@ -369,7 +369,7 @@ def main():
         agree = n_ok / n_s
         cpu = {"value": round(n_s / dt, 1), "unit": "checks/s", "cores": threads, "kind": "port",
                "sample": f"{len(host)} batches x {args.batch} checks (the timed batch + seeds 5000..), same "
-                         f"1B-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads), "
+                         f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads), "
                          f"{dt:.1f}s; every sampled check compared with the GPU result"}
 
     if rank == 0 and WL.kind == "mixed" and not args.no_oracle:
