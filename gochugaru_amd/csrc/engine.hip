@@ -63,10 +63,15 @@ struct DeviceSnapshot {
   std::vector<BaseCsr> base;
   std::vector<DevCSR> table;     // host copy of the device CSR table (base, then derived)
   std::vector<Derived> derived;  // reused by the next snapshot when the source is unchanged
-  // dispatch-graph heights (bidir.inc): reused while the row-edge CSRs and the node set are
-  std::vector<const uint32_t*> h_src;
-  std::vector<char> h_used;
+  // dispatch-graph heights per (forward node, object) (build_heights): hgt[n] = nullptr for a
+  // node without successors (height 0); hmax[n] = their maximum; h_src = the row-edge CSRs
+  // they were relaxed over (a Watch batch that changes none of them keeps them as they are)
+  std::vector<uint32_t*> hgt;
   std::vector<uint32_t> hmax;
+  std::vector<uint32_t> hcount;  // objects per hgt[n]
+  std::vector<const uint32_t*> h_src;
+  bool any_deep = false;         // some node is NF_DEEP: the grid-wide path keys entries by depth
+  const unsigned long long* d_hgt = nullptr;  // device table of hgt[n] (in the program block)
   DevNode* nodes = nullptr;
   DevItem* items = nullptr;
   DevCSR* csrs = nullptr;
@@ -74,7 +79,7 @@ struct DeviceSnapshot {
   uint32_t n_nodes = 0, n_items = 0, n_csrs = 0, n_types = 0, n_rels = 0;
   uint32_t n_fwd = 0;      // forward nodes; [n_fwd, n_nodes) is the reverse program (bidir.inc)
   bool has_bidir = false;  // some forward node is NF_BIDIR
-  uint32_t node_bits = 1, q_bits = 1;
+  uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
   uint8_t* cav_static = nullptr;  // per caveat instance (Engine::caveat_static)
   uint32_t* cav_row = nullptr;    // per caveat instance (Engine::caveat_row)
@@ -153,8 +158,12 @@ struct Ctx {
   uint64_t vmask;
   DevCounters* ctr;
   uint32_t frontier_cap, seg_cap, query_cap, join_cap;
-  uint32_t node_shift, q_shift;  // key = q << q_shift | node << node_shift | cond << 32 | obj
+  // visited key = q << q_shift | node << node_shift | (depth & depth_mask) << depth_shift |
+  // tag << 32 | obj; the depth field exists only when the snapshot has deep roots (exact-depth
+  // checks key their entries by depth), otherwise depth_mask = 0 and the tag is the cond bit
+  uint32_t node_shift, q_shift, depth_shift, depth_mask;
   uint32_t level, max_depth;
+  const unsigned long long* hgt;  // per forward node: its heights array (u32 per object) or 0
   int64_t now_us;
   // caveats (cel.hpp; gck_api.cpp caveat_table): per instance its outcome under the stored
   // context alone (0 false, 1 true, 2 partial) and, for partial ones, a row of the per-batch
@@ -181,10 +190,32 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
-__device__ __forceinline__ unsigned long long make_key(const Ctx& c, uint32_t q, uint32_t node,
-                                                       uint32_t cond, uint32_t obj) {
+// ---- exact depth semantics -----------------------------------------------
+// SpiceDB's dispatch(v, d) depends on the remaining depth d only through the depth error, and
+// monotonically: once it is not ERR at some d it keeps that value for every larger d. A check
+// whose every walk from its root stays below the budget (the root's dispatch-graph height,
+// build_heights, is < max_depth) therefore has a depth-independent answer, which the memoised
+// search (each (query, node, object) expanded once, at its minimal depth) computes. A check
+// rooted higher runs in exact-depth mode instead: its entries are keyed by depth too, so every
+// (vertex, depth) it can reach is expanded (at most max_depth + 1 per vertex, also on cyclic
+// data), and each edge whose caveat is unresolved or false starts a single-operand and-query
+// whose result goes through the oracle's and3 (a caveat-false edge still passes a depth error
+// up; a HAS below an unresolved caveat no longer masks a sibling's error).
+constexpr uint32_t kCondBit = 1u;   // Entry/Segment cond: reached through an unresolved caveat
+constexpr uint32_t kExactBit = 2u;  // ... the check runs in exact-depth mode
+constexpr uint32_t kTagNone = 0u, kTagCond = 1u, kTagFalse = 2u;  // DevQuery::operand >> 24
+
+__device__ __forceinline__ uint32_t and_tag(uint32_t tag, uint32_t res) {
+  if (tag == kTagNone || res == kResErr) return res;  // and3(_, ERR) = ERR
+  if (tag == kTagFalse || res == GCK_PERM_NO) return GCK_PERM_NO;
+  return GCK_PERM_CONDITIONAL;
+}
+
+__device__ __forceinline__ unsigned long long make_key(const Ctx& c, uint32_t q, uint32_t node, uint32_t tag,
+                                                       uint32_t depth, uint32_t obj) {
   return ((unsigned long long)q << c.q_shift) | ((unsigned long long)node << c.node_shift) |
-         ((unsigned long long)(cond & 1u) << 32) | obj;
+         ((unsigned long long)(depth & c.depth_mask) << c.depth_shift) | ((unsigned long long)(tag & 3u) << 32) |
+         obj;
 }
 
 __device__ __forceinline__ bool vlookup(const Ctx& c, unsigned long long key) {
@@ -220,13 +251,17 @@ __device__ __forceinline__ uint32_t qflags(const DevQuery* q) {
 }
 
 __device__ __forceinline__ void set_found(const Ctx& c, uint32_t q, uint32_t cond) {
-  atomicOr(&c.queries[q].flags, cond ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
+  atomicOr(&c.queries[q].flags, (cond & kCondBit) ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
 }
 
 __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node,
                                            uint32_t depth, uint32_t cond) {
-  if (cond && vlookup(c, make_key(c, q, node, 0, obj))) return;  // unconditional visit exists
-  if (vinsert(c, make_key(c, q, node, cond, obj)) <= 0) return;
+  if (cond & kExactBit) {  // exact-depth: one entry per (vertex, depth); never a cond path
+    if (vinsert(c, make_key(c, q, node, 0u, depth, obj)) <= 0) return;
+  } else {
+    if ((cond & kCondBit) && vlookup(c, make_key(c, q, node, 0u, 0u, obj))) return;  // unconditional visit exists
+    if (vinsert(c, make_key(c, q, node, cond & kCondBit, 0u, obj)) <= 0) return;
+  }
   Entry* dst = c.next;
   unsigned idx;
   if (c.world > 1 && part_owner(obj, c.world) != c.rank) {
@@ -275,6 +310,14 @@ __device__ __forceinline__ uint32_t csr_off(const DevCSR& r, uint32_t i) { retur
 __device__ __forceinline__ uint32_t csr_nbr(const DevCSR& r, uint32_t p) { return gptr(r.nbr)[p]; }
 __device__ __forceinline__ uint32_t csr_cav(const DevCSR& r, uint32_t p) { return gptr(r.cav)[p]; }
 __device__ __forceinline__ int64_t csr_exp(const DevCSR& r, uint32_t p) { return gptr(r.exp_us)[p]; }
+
+// Is the check of permission node p on object obj an exact-depth check (its root can reach the
+// depth budget)? obj must be a known object of the node's type.
+__device__ __forceinline__ bool deep_root(const Ctx& c, const DevNode* nodes, uint32_t p, uint32_t obj) {
+  if (!(nodes[p].flags & NF_DEEP) || !c.hgt) return false;
+  const unsigned long long h = gptr(c.hgt)[p];
+  return h != 0 && gptr(reinterpret_cast<const uint32_t*>(h))[obj] >= c.max_depth;
+}
 
 // lower_bound of `sid` in the CSR row of `obj`; returns the position or kNone.
 __device__ __forceinline__ uint32_t row_find(const DevCSR& r, uint32_t obj, uint32_t sid,
@@ -419,11 +462,15 @@ __device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_
 }
 
 // Spawn a join (intersection / exclusion / all-arrow) for node `node` at `obj` on behalf of
-// query `q`. Each operand becomes a child query with its own memoised frontier.
+// query `q`. Each operand becomes a child query with its own memoised frontier. `cond` carries
+// the entry's bits: the cond bit conditions the join's result (non-exact checks), the exact bit
+// passes on to the operands; an exact all() operand entered through a caveated tupleset edge is
+// tagged with the caveat's outcome (and_tag) instead of a cond bit.
 __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth,
                            uint32_t cond, uint32_t& rows) {
   const DevNode nd = c.nodes[node];
   const uint32_t check = c.queries[q].check;
+  const uint32_t ex = cond & kExactBit;
   uint32_t n_ops = 0;
   if (nd.kind == NK_ARROW_ALL) {
     bool missing = false;
@@ -438,8 +485,9 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
-          // a subject lacking the target, or one whose caveat is false, fails the all()
-          if (it.target == kNoNode || (r.is_ext && cav_state(c, csr_cav(r, p), check) == 0u)) missing = true;
+          // a subject lacking the target fails the all() (NO dominates every operand); so does
+          // one whose caveat is false, unless the check is exact-depth (and3(false, ERR) = ERR)
+          if (it.target == kNoNode || (!ex && r.is_ext && cav_state(c, csr_cav(r, p), check) == 0u)) missing = true;
           ++n_ops;
         }
       }
@@ -465,7 +513,7 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
   J.first_child = q0;
   J.n_ops = n_ops;
   J.op = nd.kind;
-  J.cond = cond;
+  J.cond = cond & kCondBit;
   J.remaining = (int32_t)n_ops;
   J.state = 0;
   J.pad = 0;
@@ -493,8 +541,13 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
         uint32_t b = csr_off(r, obj), e = csr_off(r, obj + 1);
         for (uint32_t p = b; p < e; ++p) {
           if (!visible(r, p, c.now_us)) continue;
-          const uint32_t cav = r.is_ext ? (uint32_t)(cav_state(c, csr_cav(r, p), check) == 2u) : 0u;
-          push_entry(c, q0 + k, csr_nbr(r, p), it.target, depth + 1, cav);
+          const uint32_t st = r.is_ext ? cav_state(c, csr_cav(r, p), check) : 1u;
+          if (ex) {
+            c.queries[q0 + k].operand = k | ((st == 1u ? kTagNone : st == 2u ? kTagCond : kTagFalse) << 24);
+            push_entry(c, q0 + k, csr_nbr(r, p), it.target, depth + 1, kExactBit);
+          } else {
+            push_entry(c, q0 + k, csr_nbr(r, p), it.target, depth + 1, st == 2u ? kCondBit : 0u);
+          }
           ++k;
         }
       }
@@ -502,9 +555,47 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
   } else {
     for (uint32_t k = 0; k < n_ops; ++k) {
       const DevItem it = c.items[nd.first + k];
-      push_entry(c, q0 + k, obj, it.target, depth + it.dispatch, 0u);
+      push_entry(c, q0 + k, obj, it.target, depth + it.dispatch, ex);
     }
   }
+}
+
+// Exact-depth checks: the edge into (obj, node) has a caveat that is unresolved (kTagCond) or
+// false (kTagFalse) for this check: a single-operand join whose operand query walks from
+// (obj, node) and whose result reaches query q through and_tag. Deduplicated per (q, vertex,
+// depth, tag).
+__device__ void spawn_and(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth, uint32_t tag) {
+  if (vinsert(c, make_key(c, q, node, tag, depth, obj)) <= 0) return;
+  unsigned j = atomicAdd(&c.ctr->n_joins, 1u);
+  unsigned q0 = atomicAdd(&c.ctr->n_queries, 1u);
+  if (j >= c.join_cap) {
+    atomicOr(&c.ctr->overflow, 16u);
+    return;
+  }
+  if (q0 + 1 > c.query_cap) {
+    atomicOr(&c.ctr->overflow, 8u);
+    return;
+  }
+  DevJoin J;
+  J.parent_q = q;
+  J.first_child = q0;
+  J.n_ops = 1;
+  J.op = NK_INTERSECT;  // the intersection of one operand is the operand
+  J.cond = 0;
+  J.remaining = 1;
+  J.state = 0;
+  J.pad = 0;
+  c.joins[j] = J;
+  DevQuery cq;
+  cq.check = c.queries[q].check;
+  cq.parent_join = j;
+  cq.flags = 0;
+  cq.pending_joins = 0;
+  cq.last_alive = c.level;
+  cq.operand = tag << 24;
+  c.queries[q0] = cq;
+  __hip_atomic_fetch_add(&c.queries[q].pending_joins, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  push_entry(c, q0, obj, node, depth, kExactBit);
 }
 
 // ---- kernels -----------------------------------------------------------------------------
@@ -560,7 +651,7 @@ __global__ void __launch_bounds__(kBlock) k_init(Ctx c, const gck_item* __restri
   e.obj = it.resource_id;
   e.node = it.permission;
   e.depth = 0;
-  e.cond = 0;
+  e.cond = (!(q.flags & QF_DONE) && deep_root(c, c.nodes, it.permission, it.resource_id)) ? kExactBit : 0u;
   fr0[i] = e;
 }
 
@@ -598,7 +689,7 @@ __global__ void __launch_bounds__(kBlock) k_expand(Ctx c, const Entry* __restric
                 if (ci == kNone) continue;
                 const uint32_t m = member_test(c, c.csrs[ci], e.obj, s.sid, direct, wild, q->check, rows, probes);
                 if (m) {
-                  const uint32_t cond = e.cond | (m == 2);
+                  const uint32_t cond = (e.cond & kCondBit) | (m == 2);
                   set_found(c, e.q, cond);
                   if (!cond) done = true;
                 }
@@ -670,9 +761,17 @@ __global__ void __launch_bounds__(kBlock) k_edges(Ctx c) {
     uint32_t cond = s.cond;
     if (r.is_ext) {
       ++ext_edges;
-      const uint32_t st = ext_state(c, r, p, c.queries[s.q].check);
-      if (st == 0u) continue;
-      cond |= (st == 2u);
+      if (!visible(r, p, c.now_us)) continue;
+      const uint32_t st = cav_state(c, csr_cav(r, p), c.queries[s.q].check);
+      if (cond & kExactBit) {
+        if (st != 1u) {  // unresolved or false caveat: an and-query (and3 of the oracle)
+          if (x != kWildcard) spawn_and(c, s.q, x, s.target, s.depth, st == 2u ? kTagCond : kTagFalse);
+          continue;
+        }
+      } else {
+        if (st == 0u) continue;
+        cond |= (st == 2u);
+      }
     }
     if (x == kWildcard) continue;
     push_entry(c, s.q, x, s.target, s.depth, cond);
@@ -708,16 +807,18 @@ __device__ void finalize(const Ctx& c, uint32_t qi, uint32_t res) {
     if (j == kNone) return;
     DevJoin* J = &c.joins[j];
     const uint32_t op = J->op;
+    const uint32_t opnd = q->operand;
+    const uint32_t r = and_tag(opnd >> 24, res);  // the operand's contribution
     uint32_t bit;
     bool early;
-    if (op == NK_EXCLUDE && q->operand == 0) {
-      bit = res == GCK_PERM_HAS ? JS_BASE_Y : res == GCK_PERM_NO ? JS_BASE_N
-            : res == GCK_PERM_CONDITIONAL ? JS_BASE_C : JS_BASE_ERR;
-      early = res == GCK_PERM_NO;
+    if (op == NK_EXCLUDE && (opnd & 0xFFFFFFu) == 0) {
+      bit = r == GCK_PERM_HAS ? JS_BASE_Y : r == GCK_PERM_NO ? JS_BASE_N
+            : r == GCK_PERM_CONDITIONAL ? JS_BASE_C : JS_BASE_ERR;
+      early = r == GCK_PERM_NO;
     } else {
-      bit = res == GCK_PERM_HAS ? JS_ANY_Y : res == GCK_PERM_NO ? JS_ANY_N
-            : res == GCK_PERM_CONDITIONAL ? JS_ANY_C : JS_ANY_ERR;
-      early = (op == NK_EXCLUDE) ? res == GCK_PERM_HAS : res == GCK_PERM_NO;
+      bit = r == GCK_PERM_HAS ? JS_ANY_Y : r == GCK_PERM_NO ? JS_ANY_N
+            : r == GCK_PERM_CONDITIONAL ? JS_ANY_C : JS_ANY_ERR;
+      early = (op == NK_EXCLUDE) ? r == GCK_PERM_HAS : r == GCK_PERM_NO;
     }
     __hip_atomic_fetch_or(&J->state, bit, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     int rem = __hip_atomic_fetch_add(&J->remaining, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) - 1;
@@ -1056,13 +1157,14 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
   d.has_wild = hw ? 1 : 0;
 }
 
+#include "heights.inc"
 #include "bidir.inc"
 
 // Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
 // (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
 // derived structures of unchanged CSRs. Taken-over arrays join the new snapshot's allocation
 // list only on success, so a failure frees nothing the previous snapshot still owns.
-void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
+void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
   Schema& sc = *e.schema;
@@ -1152,6 +1254,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
       }
     }
     std::vector<DevNode> nodes = sc.nodes;
+    build_heights(e, *ds, nodes, items, table, info, adopted, delta);
     build_bidir(e, *ds, nodes, items, table, info, adopted);
     for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
       if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
@@ -1184,6 +1287,9 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     const size_t o_counts = put(counts.data(), counts.size() * 4);
     const size_t o_cst = put(cst.data(), cst.size());
     const size_t o_crow = put(crow.data(), crow.size() * 4);
+    std::vector<unsigned long long> hp(ds->hgt.size());  // heights array of each forward node
+    for (size_t n = 0; n < hp.size(); ++n) hp[n] = (unsigned long long)(uintptr_t)ds->hgt[n];
+    const size_t o_hgt = put(hp.data(), hp.size() * 8);
     unsigned char* d_blob = dalloc<unsigned char>(ds->allocs, blob.size(), &ds->bytes);
     HIP_OK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
     ds->nodes = reinterpret_cast<DevNode*>(d_blob + o_nodes);
@@ -1192,9 +1298,13 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs) {
     ds->type_counts = reinterpret_cast<uint32_t*>(d_blob + o_counts);
     ds->cav_static = d_blob + o_cst;
     ds->cav_row = reinterpret_cast<uint32_t*>(d_blob + o_crow);
+    ds->d_hgt = reinterpret_cast<const unsigned long long*>(d_blob + o_hgt);
     ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
     if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
     ds->q_bits = 31 - ds->node_bits;
+    // exact-depth layout (make_ctx): tag 2 bits, depth, node, query id below bit 63
+    const uint32_t md = e.cfg.max_depth ? e.cfg.max_depth : 50;
+    ds->q_bits_deep = 63 - (34 + ceil_log2((uint64_t)md + 1) + ds->node_bits);
   } catch (...) {
     free_list(ds->allocs);
     delete ds;
@@ -1343,12 +1453,23 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.ctr = w.ctr;
   c.frontier_cap = (uint32_t)w.frontier_cap;
   c.seg_cap = (uint32_t)std::min<size_t>(w.seg_cap, (1u << 24) - 1);
-  uint32_t qcap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << ds.q_bits);
+  const uint32_t q_bits = ds.any_deep ? ds.q_bits_deep : ds.q_bits;
+  uint32_t qcap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << q_bits);
   c.query_cap = qcap;
   c.join_cap = (uint32_t)w.join_cap;
-  c.node_shift = 33;
-  c.q_shift = 33 + ds.node_bits;
   c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
+  if (ds.any_deep) {  // exact-depth checks key their entries by depth (make_key)
+    const uint32_t db = ceil_log2((uint64_t)c.max_depth + 1);
+    c.depth_shift = 34;
+    c.depth_mask = (1u << db) - 1u;
+    c.node_shift = 34 + db;
+  } else {
+    c.depth_shift = 0;
+    c.depth_mask = 0;
+    c.node_shift = 33;
+  }
+  c.q_shift = c.node_shift + ds.node_bits;
+  c.hgt = ds.d_hgt;
   c.now_us = now_us;
   c.cav_static = ds.cav_static;
   c.cav_row = ds.cav_row;

@@ -186,7 +186,9 @@ std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>&
 
 // engine.hip
 int device_init(Engine& e);
-void device_upload(Engine& e, std::vector<HostCSR>& csrs);
+// delta: a Watch-batch re-link (delta.inc): derived structures of unchanged CSRs and the
+// previous heights are taken over
+void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta = false);
 void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
 // cav_table: the call's caveat outcome table (row = partial instance, n_ctx columns = check
 // contexts 1..n_ctx; empty when the call has no check contexts)

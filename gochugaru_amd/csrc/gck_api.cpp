@@ -140,6 +140,10 @@ int gck_create(const gck_config* cfg, gck_engine** out) {
       delete e;
       throw Error(GCK_E_INVALID_ARGUMENT, "bad device ordinal");
     }
+    if (e->impl.cfg.max_depth > 250) {  // frontier entries hold the depth in 8 bits
+      delete e;
+      throw Error(GCK_E_INVALID_ARGUMENT, "max_depth above 250");
+    }
     reset_caveats(e->impl);
     *out = e;
   });

@@ -47,6 +47,8 @@ enum NodeFlags : uint8_t {
   NF_REAL = 1,   // a schema relation/permission: the identity filter applies
   NF_BIDIR = 2,  // a forward node whose checks may run bidirectionally (engine.hip build_bidir)
   NF_JUMP = 4,   // a reverse node whose first item is an ancestor-closure jump (bidir.inc)
+  NF_DEEP = 8,   // a forward node some of whose objects can reach the depth budget (heights,
+                 // engine.hip build_heights): a check rooted at such an object runs exact-depth
 };
 
 enum ItemKind : uint8_t {
@@ -126,7 +128,9 @@ struct DevQuery {
   uint32_t flags;        // QueryFlags (atomic)
   int32_t pending_joins; // joins spawned and not resolved (atomic)
   uint32_t last_alive;   // last level an entry for this query was pushed into
-  uint32_t operand;      // operand index inside the parent join
+  uint32_t operand;      // operand index inside the parent join (bits 0..23) | caveat tag << 24:
+                         // how the result combines with the caveat of the edge the operand was
+                         // entered through (exact-depth checks; engine.hip and_tag)
 };
 
 enum JoinState : uint32_t {
@@ -157,7 +161,7 @@ struct Entry {  // 12 B frontier record
   uint32_t obj;
   uint16_t node;
   uint8_t depth;
-  uint8_t cond;
+  uint8_t cond;  // bit 0: reached through an unresolved caveat; bit 1: exact-depth check
 };
 
 struct Segment {  // one CSR row range to enumerate

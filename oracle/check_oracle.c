@@ -17,9 +17,13 @@
  * Parity pinning: cross-checked against spicedb_ref.py (itself pinned by the reference's
  * known answers, tests/golden) on seeded graphs in tests/test_c_oracle.py.
  *
- * Per-check memo: results that are not ERR are depth-independent (a NO/COND result means the
- * sub-graph was explored without truncation; a HAS stays HAS with more budget), so they are
- * memoised per check; ERR results are recomputed.
+ * Per-check memo, exact under the depth budget: for a fixed check, dispatch(v, d) is a pure
+ * function of the vertex v and the remaining depth d, and it is monotone in d — once it is not
+ * ERR at some d it keeps that value at every larger d (by induction over the tri-state algebra:
+ * only an ERR operand can change when the budget grows, and a non-ERR result never depends on
+ * an ERR operand). So the memo keeps, per vertex, the non-ERR value with the smallest depth it
+ * was seen at and the largest depth seen to give ERR, and answers a lookup at d from whichever
+ * bound covers d. Cyclic and re-converging data stay polynomial (|vertices| x depth).
  *
  * Input: a relation/permission program (int32 stream, built by oracle/corc.py from the
  * oracle's own schema parser) and per-(relation, subject kind) CSR arrays.
@@ -76,7 +80,9 @@ typedef struct {
   /* memo: open addressing keyed by (rel, obj) with a generation stamp */
   uint64_t* keys;
   uint32_t* gen;
-  uint8_t* val;
+  uint8_t* val;  /* non-ERR value (0 = none known) */
+  uint8_t* okd;  /* ... known from this remaining depth upwards */
+  uint8_t* errd; /* ERR known at every remaining depth <= errd (0 = none known) */
   uint32_t cap, mask, cur_gen, used;
   /* subject */
   uint32_t sid;
@@ -110,29 +116,42 @@ static uint64_t mix64(uint64_t x) {
   return x;
 }
 
-static int memo_get(orc_ctx* c, uint64_t key) {
+/* the memo answer for (key, remaining depth dr): a value, ERR, or 0 = unknown */
+static int memo_get(orc_ctx* c, uint64_t key, int dr) {
   uint32_t h = (uint32_t)mix64(key) & c->mask;
   for (;;) {
     if (c->gen[h] != c->cur_gen) return 0;
-    if (c->keys[h] == key) return c->val[h];
+    if (c->keys[h] == key) {
+      if (c->val[h] && dr >= c->okd[h]) return c->val[h];
+      if (dr <= c->errd[h]) return ERR;
+      return 0;
+    }
     h = (h + 1) & c->mask;
   }
 }
 
-static void memo_put(orc_ctx* c, uint64_t key, int v) {
-  if (c->used * 2 >= c->cap) return; /* full enough: stop memoising this check */
+static void memo_put(orc_ctx* c, uint64_t key, int v, int dr) {
   uint32_t h = (uint32_t)mix64(key) & c->mask;
   while (c->gen[h] == c->cur_gen) {
-    if (c->keys[h] == key) {
-      c->val[h] = (uint8_t)v;
-      return;
-    }
+    if (c->keys[h] == key) break;
     h = (h + 1) & c->mask;
   }
-  c->gen[h] = c->cur_gen;
-  c->keys[h] = key;
-  c->val[h] = (uint8_t)v;
-  c->used++;
+  if (c->gen[h] != c->cur_gen) {
+    if (c->used * 2 >= c->cap) return; /* full enough: stop adding keys for this check */
+    c->gen[h] = c->cur_gen;
+    c->keys[h] = key;
+    c->val[h] = 0;
+    c->okd[h] = 255;
+    c->errd[h] = 0;
+    c->used++;
+  }
+  if (dr > 255) dr = 255;
+  if (v == ERR) {
+    if (dr > c->errd[h]) c->errd[h] = (uint8_t)dr;
+  } else if (!c->val[h] || dr < c->okd[h]) {
+    c->val[h] = (uint8_t)v;
+    c->okd[h] = (uint8_t)dr;
+  }
 }
 
 static int row_find(orc_ctx* c, const orc_csr* r, uint32_t obj, uint32_t sid, uint32_t* pos) {
@@ -341,7 +360,7 @@ static int dispatch(const orc_program* p, orc_ctx* c, int type, uint32_t obj, in
   if (dr <= 0) return ERR;
   if (type == c->stype && rel == c->srel && obj == c->sid) return HAS;
   uint64_t key = ((uint64_t)(uint32_t)rel << 32) | obj;
-  int m = memo_get(c, key);
+  int m = memo_get(c, key, dr);
   if (m) return m;
   int v;
   if (rel_is_perm(p, rel)) {
@@ -350,7 +369,7 @@ static int dispatch(const orc_program* p, orc_ctx* c, int type, uint32_t obj, in
   } else {
     v = check_direct(p, c, rel, obj, dr);
   }
-  if (v != ERR) memo_put(c, key, v);
+  memo_put(c, key, v, dr);
   return v;
 }
 
@@ -389,6 +408,8 @@ int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, s
     c.keys = (uint64_t*)malloc(sizeof(uint64_t) * c.cap);
     c.gen = (uint32_t*)calloc(c.cap, sizeof(uint32_t));
     c.val = (uint8_t*)malloc(c.cap);
+    c.okd = (uint8_t*)malloc(c.cap);
+    c.errd = (uint8_t*)malloc(c.cap);
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 64)
 #endif
@@ -420,6 +441,8 @@ int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, s
     free(c.keys);
     free(c.gen);
     free(c.val);
+    free(c.okd);
+    free(c.errd);
   }
   if (counters) {
     counters[0] = rows;
@@ -466,6 +489,8 @@ int orc_count_bfs(const int32_t* prog, const orc_csr* csrs, const orc_item* item
     c.keys = (uint64_t*)malloc(sizeof(uint64_t) * c.cap);
     c.gen = (uint32_t*)calloc(c.cap, sizeof(uint32_t));
     c.val = (uint8_t*)malloc(c.cap);
+    c.okd = (uint8_t*)malloc(c.cap);
+    c.errd = (uint8_t*)malloc(c.cap);
     size_t fcap = 1 << 16;
     orc_node* cur = (orc_node*)malloc(sizeof(orc_node) * fcap);
     orc_node* nxt = (orc_node*)malloc(sizeof(orc_node) * fcap);
@@ -499,8 +524,8 @@ int orc_count_bfs(const int32_t* prog, const orc_csr* csrs, const orc_item* item
 #define PUSH(o, r)                                                           \
   do {                                                                       \
     uint64_t key_ = ((uint64_t)(uint32_t)(r) << 32) | (o);                   \
-    if (!memo_get(&c, key_)) {                                               \
-      memo_put(&c, key_, 1);                                                 \
+    if (!memo_get(&c, key_, 255)) {                                          \
+      memo_put(&c, key_, 1, 0);                                              \
       if (nn == ncap) {                                                      \
         ncap *= 2;                                                           \
         nxt = (orc_node*)realloc(nxt, sizeof(orc_node) * ncap);              \
@@ -585,6 +610,8 @@ int orc_count_bfs(const int32_t* prog, const orc_csr* csrs, const orc_item* item
     free(c.keys);
     free(c.gen);
     free(c.val);
+    free(c.okd);
+    free(c.errd);
     free(cur);
     free(nxt);
   }

@@ -1005,6 +1005,10 @@ class Checker:
             return 0, err
         self._subj = (it.subject_type, it.subject_id, it.subject_relation or ELLIPSIS)
         self._ctx = dict(it.context or {})
+        # Memo of dispatch results keyed by (vertex, remaining depth): for a fixed subject,
+        # context and clock, _dispatch is a pure function of its arguments, so this changes no
+        # result — it only keeps cyclic and re-converging data polynomial (|vertices| x depth).
+        self._memo = {}
         r = self._dispatch(it.resource_type, it.resource_id, it.permission, self.max_depth)
         if r == ERR:
             return 0, ITEM_ERR_MAX_DEPTH
@@ -1022,9 +1026,15 @@ class Checker:
         r = self.schema.relation(rtype, rel)
         if r is None:
             return NO
-        if r.is_permission:
-            return self._eval(r.expr, rtype, rid, depth_remaining)
-        return self._check_direct(rtype, rid, rel, depth_remaining)
+        key = (rtype, rid, rel, depth_remaining)
+        v = self._memo.get(key)
+        if v is None:
+            if r.is_permission:
+                v = self._eval(r.expr, rtype, rid, depth_remaining)
+            else:
+                v = self._check_direct(rtype, rid, rel, depth_remaining)
+            self._memo[key] = v
+        return v
 
     def _visible(self, t: Tuple_) -> bool:
         return t.expires_at is None or t.expires_at > self.now

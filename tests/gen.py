@@ -1,6 +1,8 @@
 """Seeded synthetic schemas + relationship graphs for parity tests (small sizes: the Python
-oracle must finish in seconds). Every graph is acyclic so that parity is well-defined
-(SURVEY.md §5.1 item 9)."""
+oracle must finish in seconds). Most families are acyclic and far below the depth budget;
+``cyclic`` and ``near_budget`` exercise SpiceDB's depth semantics:
+cyclic userset / arrow data, caveats on the way into cycles, and re-converging paths that
+straddle a small budget (FAMILY_DEPTH)."""
 import random
 
 GDOCS = """
@@ -292,6 +294,130 @@ def gdocs_deep(seed, n_users=80, n_groups=40, n_folders=40, n_docs=60):
     return GDOCS, t, checks
 
 
+CYCLIC = """
+caveat only_on_tuesday(day_of_the_week string) {
+  day_of_the_week == "tuesday"
+}
+definition user {}
+definition group {
+  relation member: user | group#member | user with only_on_tuesday | group#member with only_on_tuesday
+}
+definition folder {
+  relation parent: folder | folder with only_on_tuesday
+  relation viewer: user | group#member
+  relation banned: user | group#member
+  permission view = (viewer + parent->view) - banned
+  permission every = parent.all(view)
+}
+definition doc {
+  relation parent: folder
+  relation viewer: user | group#member | group#member with only_on_tuesday
+  relation editor: user | group#member
+  permission edit = editor + parent->view
+  permission view = viewer + edit
+  permission strict = viewer & edit
+}
+"""
+
+
+def cyclic(seed, n_users=30, n_groups=18, n_folders=16, n_docs=30):
+    """Cyclic group membership and folder parents (self-loops included), some of the cycle
+    edges caveated: a check that never reaches its subject ends in the depth error, one that
+    reaches it first is HAS, and a caveat on the way into a cycle must not hide the error
+    (and3(false, ERR) = ERR in the oracle)."""
+    rng = random.Random(seed)
+    t = []
+    tue = "[only_on_tuesday]"
+    for g in range(n_groups):
+        for _ in range(rng.randint(0, 2)):
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}" + (tue if rng.random() < 0.2 else ""))
+        for _ in range(rng.randint(0, 2)):
+            h = _pick(rng, n_groups)  # any direction: cycles and self-loops
+            t.append(f"group:g{g}#member@group:g{h}#member" + (tue if rng.random() < 0.25 else ""))
+    for f in range(n_folders):
+        for _ in range(rng.randint(0, 2)):
+            t.append(f"folder:f{f}#parent@folder:f{_pick(rng, n_folders)}" + (tue if rng.random() < 0.2 else ""))
+        for rel in ("viewer", "banned"):
+            for _ in range(rng.randint(0, 1 if rel == "banned" else 2)):
+                if rng.random() < 0.5:
+                    t.append(f"folder:f{f}#{rel}@user:u{_pick(rng, n_users)}")
+                else:
+                    t.append(f"folder:f{f}#{rel}@group:g{_pick(rng, n_groups)}#member")
+    for d in range(n_docs):
+        if rng.random() < 0.7:
+            t.append(f"doc:d{d}#parent@folder:f{_pick(rng, n_folders)}")
+        for rel in ("viewer", "editor"):
+            for _ in range(rng.randint(0, 2)):
+                x = rng.random()
+                if x < 0.4:
+                    t.append(f"doc:d{d}#{rel}@user:u{_pick(rng, n_users)}")
+                elif x < 0.8 or rel == "editor":
+                    t.append(f"doc:d{d}#{rel}@group:g{_pick(rng, n_groups)}#member")
+                else:
+                    t.append(f"doc:d{d}#viewer@group:g{_pick(rng, n_groups)}#member{tue}")
+    t = sorted(set(t))
+    checks = []
+    for _ in range(300):
+        x = rng.random()
+        if x < 0.4:
+            checks.append(f"doc:d{_pick(rng, n_docs + 2)}#{rng.choice(['view', 'edit', 'strict'])}@user:u{_pick(rng, n_users + 2)}")
+        elif x < 0.65:
+            checks.append(f"folder:f{_pick(rng, n_folders)}#{rng.choice(['view', 'every'])}@user:u{_pick(rng, n_users)}")
+        elif x < 0.85:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@user:u{_pick(rng, n_users)}")
+        elif x < 0.93:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@group:g{_pick(rng, n_groups)}#member")
+        else:
+            checks.append(f"doc:d{_pick(rng, n_docs)}#view@group:g{_pick(rng, n_groups)}#member")
+    return CYCLIC, t, checks
+
+
+def near_budget(seed, n_users=40, n_groups=48, n_folders=24, n_docs=40):
+    """Acyclic, but with re-converging paths of different lengths around a small depth budget
+    (FAMILY_DEPTH: 8): a vertex is reachable both within and beyond the budget, so the answer
+    depends on SpiceDB's exact depth accounting (every dispatch path counts, not the shortest)."""
+    rng = random.Random(seed)
+    t = []
+    for g in range(n_groups):  # chains g -> g+1 (long paths) plus skips g -> g+k (short ones)
+        for _ in range(rng.randint(0, 2)):
+            t.append(f"group:g{g}#member@user:u{_pick(rng, n_users)}")
+        if g + 1 < n_groups and rng.random() < 0.85:
+            t.append(f"group:g{g}#member@group:g{g + 1}#member")
+        if rng.random() < 0.4:
+            h = g + rng.randint(2, 6)
+            if h < n_groups:
+                t.append(f"group:g{g}#member@group:g{h}#member")
+    for f in range(n_folders):
+        if f > 0 and rng.random() < 0.9:
+            t.append(f"folder:f{f}#parent@folder:f{f - 1}")
+        if f > 2 and rng.random() < 0.3:
+            t.append(f"folder:f{f}#parent@folder:f{f - rng.randint(2, 3)}")
+        if rng.random() < 0.5:
+            t.append(f"folder:f{f}#viewer@group:g{_pick(rng, n_groups)}#member")
+        if rng.random() < 0.3:
+            t.append(f"folder:f{f}#editor@user:u{_pick(rng, n_users)}")
+    for d in range(n_docs):
+        t.append(f"doc:d{d}#parent@folder:f{_pick(rng, n_folders)}")
+        if rng.random() < 0.5:
+            t.append(f"doc:d{d}#viewer@group:g{_pick(rng, n_groups)}#member")
+        if rng.random() < 0.3:
+            t.append(f"doc:d{d}#editor@user:u{_pick(rng, n_users)}")
+    t = sorted(set(t))
+    checks = []
+    for _ in range(300):
+        x = rng.random()
+        if x < 0.5:
+            checks.append(f"doc:d{_pick(rng, n_docs)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users)}")
+        elif x < 0.75:
+            checks.append(f"folder:f{_pick(rng, n_folders)}#{rng.choice(['view', 'edit'])}@user:u{_pick(rng, n_users)}")
+        else:
+            checks.append(f"group:g{_pick(rng, n_groups)}#member@user:u{_pick(rng, n_users)}")
+    return GDOCS_NOWILD, t, checks
+
+
+GDOCS_NOWILD = GDOCS.replace("relation viewer: user | user:* | group#member", "relation viewer: user | group#member")
+
+
 def check_contexts(seed, n):
     """Check-time caveat contexts for n checks (CheckBulkPermissionsRequestItem.Context):
     none, a satisfying one or a failing one for only_on_tuesday, and an unrelated key."""
@@ -301,5 +427,7 @@ def check_contexts(seed, n):
 
 
 FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested,
-            "gdocs_deep": gdocs_deep}
+            "gdocs_deep": gdocs_deep, "cyclic": cyclic, "near_budget": near_budget}
+# the dispatch depth budget a family is checked under (default: SpiceDB's 50)
+FAMILY_DEPTH = {"near_budget": 8}
 NOW_US = 1759449600 * 1_000_000  # 2025-10-03T00:00:00Z

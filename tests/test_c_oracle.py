@@ -29,7 +29,8 @@ def run_both(schema, tuples, checks, now=0.0, max_depth=50, threads=1):
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_c_oracle_matches_python_oracle(family, seed):
     schema, tuples, checks = gen.FAMILIES[family](seed)
-    want, got = run_both(schema, tuples, checks, now=gen.NOW_US / 1e6, threads=2)
+    want, got = run_both(schema, tuples, checks, now=gen.NOW_US / 1e6, threads=2,
+                         max_depth=gen.FAMILY_DEPTH.get(family, 50))
     bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
     assert not bad, bad[:10]
 

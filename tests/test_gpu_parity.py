@@ -199,15 +199,17 @@ PATHS = {
 def test_random_parity(family, seed, path):
     schema, tuples, checks = gen.FAMILIES[family](seed)
     contexts = gen.check_contexts(seed, len(checks))
-    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    depth = gen.FAMILY_DEPTH.get(family, 50)
+    ck = oracle_for(schema, tuples, max_depth=depth, now=gen.NOW_US / 1e6)
     want = [ck.check(to_oracle_item(parse_check(c), x)) for c, x in zip(checks, contexts)]
-    e = make_engine(schema, tuples, **PATHS[path])
+    e = make_engine(schema, tuples, max_depth=depth, **PATHS[path])
     got = device_results(e, checks, now_us=gen.NOW_US, contexts=contexts)
     bad = [(c, w, g) for c, w, g in zip(checks, want, got) if w != g]
     assert not bad, bad[:10]
+    deep = family in ("cyclic", "near_budget")  # roots that may hit the budget take the exact path
     if path == "bundle-deferred" and family != "caveated":  # caveated graphs are too small to overflow
         assert e.stats()["deferred"] > 0
-    if path == "bundle":
+    if path == "bundle" and not deep:
         assert e.stats()["deferred"] == 0
     if path == "bundle" and family in ("nested", "gdocs_deep"):
         assert e.stats()["bidir_checks"] > 0
