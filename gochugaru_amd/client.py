@@ -135,10 +135,13 @@ class Client:
         rels = [r.Relationship() for r in rs]
         try:
             requirement, revision = _requirement(cs)
-            items, contexts = self.engine.make_request(rels)
-            perm, err = retryRetriableErrors(
-                ctx or Background,
-                lambda: self.engine.check_bulk(items, requirement, revision, contexts=contexts))
+
+            def attempt():
+                # interned per attempt, like the server resolving names at evaluation time: an
+                # object a Watch batch created while this request waited is found on the retry
+                items, contexts = self.engine.make_request(rels)
+                return self.engine.check_bulk(items, requirement, revision, contexts=contexts)
+            perm, err = retryRetriableErrors(ctx or Background, attempt)
         except Exception as e:  # noqa: BLE001 — Go returns (nil, err)
             return None, e
         results: List[bool] = []
@@ -251,6 +254,12 @@ class Client:
         self.engine.load_schema(schema)
         lines = "\n".join(r.String() if hasattr(r, "String") else str(r) for r in relationships)
         self.engine.load_snapshot_text(revision, lines)
+
+    def SetHeadRevision(self, revision: int) -> None:
+        """The source's head revision that ``consistency.Full()`` must reach (consistency/
+        consistency.go:25-35): ReadSchema's ReadAt token (client/client.go:416-422) or a Watch
+        checkpoint. Until ApplyUpdates reaches it, a Full check is Unavailable and retried."""
+        self.engine.set_head_revision(revision)
 
     _UPDATE_OPS = {_rel.UpdateCreate: "CREATE", _rel.UpdateTouch: "TOUCH", _rel.UpdateDelete: "DELETE"}
 

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -87,10 +88,33 @@ struct DeviceSnapshot {
 
 struct PartState;  // partition.inc
 
+// One check workspace: the scratch of one batch in flight, on its own HIP stream. An engine
+// keeps a pool of them (acquire_ws / release_ws), so concurrent callers — and the batches a
+// caller submits without waiting (gck_check_submit) — run side by side on the device: the
+// persistent bundle kernels of the next batch fill the tail of the previous one.
 struct Workspace {
-  PartState* part = nullptr;  // partitioned batch in progress (partition.inc)
+  PartState* part = nullptr;  // partitioned batch in progress (partition.inc; Engine::part_ws only)
+  bool busy = false;          // taken from the pool (Engine::ws_mu)
   size_t max_batch = 0, frontier_cap = 0, seg_cap = 0, query_cap = 0, join_cap = 0;
   uint64_t visited_cap = 0;
+  // ---- the batch in flight (submit_batch .. finish_batch); guarded by `m` -----------------
+  std::mutex m;
+  int state = 0;              // 0 idle, 1 stage A submitted, 2 finished (results written)
+  int fail_code = 0;          // a failure while a writer drained the batch (drain_batches)
+  std::string fail_msg;
+  hipStream_t b_st = nullptr; // the stream the batch runs on
+  const gck_item* b_items = nullptr;
+  uint32_t b_n = 0;
+  int64_t b_now = 0;
+  uint8_t* b_dperm = nullptr; // device results
+  int32_t* b_derr = nullptr;
+  uint8_t* b_hperm = nullptr; // host batch: the caller's result buffers (copied out by the wait)
+  int32_t* b_herr = nullptr;
+  bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
+  unsigned b_seq = 0;         // publish sequence of stage A
+  float b_ms = 0.f;
+  // ---- grid-wide path (allocated on first use: ensure_wide) --------------------------------
+  bool wide_ready = false;
   DevCheck* checks = nullptr;
   int32_t* item_err = nullptr;
   DevQuery* queries = nullptr;
@@ -98,6 +122,7 @@ struct Workspace {
   Entry* fr[2] = {nullptr, nullptr};
   Segment* segs = nullptr;
   unsigned long long* visited = nullptr;
+  // ---- counters, publication, staging ------------------------------------------------------
   DevCounters* ctr = nullptr;
   DevCounters* h_ctr = nullptr;  // pinned, coherent (k_publish writes it)
   unsigned* h_seq = nullptr;     // after h_ctr + bundle counters: the last published batch
@@ -107,10 +132,13 @@ struct Workspace {
   gck_item* d_items = nullptr;   // staging for the host-buffer API
   uint8_t* d_perm = nullptr;
   int32_t* d_err = nullptr;
-  hipStream_t stream = nullptr;
+  gck_item* h_items = nullptr;   // pinned staging of a host batch: items in, results out
+  uint8_t* h_perm = nullptr;
+  int32_t* h_err = nullptr;
+  hipStream_t stream = nullptr;  // the workspace's own stream (host batches, lookups)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // GCK_FLAG_PROFILE
-  // bundle path
+  // ---- bundle path -------------------------------------------------------------------------
   uint32_t b_checks = 16, b_fc = 4096, b_vslots = 16384, b_blocks = 0;
   unsigned long long* b_fr = nullptr;  // packed frontier entries beyond the LDS part
   unsigned long long* b_vis = nullptr;
@@ -119,7 +147,8 @@ struct Workspace {
   unsigned* b_ctrs = nullptr;      // [0] bundle ctr, [1] deferred, [2] giant bundle ctr, [3] deferred2
   unsigned* h_bctrs = nullptr;     // pinned
   uint32_t b_budget = 1024;
-  // giant-check stage: one 16-wave workgroup per bundle
+  // giant-check stage: one 16-wave workgroup per bundle (allocated on first use: ensure_giant)
+  bool giant_ready = false;
   uint32_t g_fc = 65536, g_vslots = 262144, g_slots = 0;
   unsigned long long* g_fr = nullptr;
   unsigned long long* g_vis = nullptr;
@@ -136,6 +165,11 @@ struct Workspace {
   uint32_t* lk_ids = nullptr;
   uint8_t* lk_perm = nullptr;
   unsigned* lk_cnt = nullptr;
+  // GCK_DEBUG_BUNDLE / GCK_DEBUG_TIMING buffers (per workspace: engines on several devices in
+  // one process, and concurrent batches, never share one)
+  uint32_t* dbg = nullptr;
+  unsigned long long* timing = nullptr;
+  size_t timing_cap = 0;
   std::vector<void*> allocs;
 };
 
@@ -1055,6 +1089,24 @@ static void free_list(std::vector<void*>& list) {
 static void free_part(PartState* p);  // partition.inc
 static void partition_filter(const Engine& e, DeviceSnapshot& ds, DevCSR& d, uint64_t& ne);
 
+static void free_workspace(Workspace* w) {
+  if (w->stream) (void)hipStreamSynchronize(w->stream);
+  if (w->b_st && w->state == 1) (void)hipStreamSynchronize(w->b_st);  // a batch never waited for
+  free_part(w->part);
+  free_list(w->allocs);
+  if (w->h_ctr) (void)hipHostFree(w->h_ctr);
+  if (w->h_items) (void)hipHostFree(w->h_items);
+  if (w->dbg) (void)hipFree(w->dbg);
+  if (w->timing) (void)hipFree(w->timing);
+  if (w->ev0) (void)hipEventDestroy(w->ev0);
+  if (w->ev1) (void)hipEventDestroy(w->ev1);
+  if (w->ev2) (void)hipEventDestroy(w->ev2);
+  for (hipEvent_t ev : w->pev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (w->stream) (void)hipStreamDestroy(w->stream);
+  delete w;
+}
+
 void device_free(Engine& e) {
   if (e.delta_scratch) {
     (void)hipSetDevice(e.device);
@@ -1068,20 +1120,13 @@ void device_free(Engine& e) {
     delete e.dev;
     e.dev = nullptr;
   }
-  if (e.ws) {
+  if (!e.ws_pool.empty() || e.part_ws) {
     (void)hipSetDevice(e.device);
-    Workspace* w = e.ws;
-    free_part(w->part);
-    free_list(w->allocs);
-    if (w->h_ctr) (void)hipHostFree(w->h_ctr);
-    if (w->ev0) (void)hipEventDestroy(w->ev0);
-    if (w->ev1) (void)hipEventDestroy(w->ev1);
-    if (w->ev2) (void)hipEventDestroy(w->ev2);
-    for (hipEvent_t ev : w->pev)
-      if (ev) (void)hipEventDestroy(ev);
-    if (w->stream) (void)hipStreamDestroy(w->stream);
-    delete w;
-    e.ws = nullptr;
+    std::vector<Workspace*> all = e.ws_pool;
+    if (e.part_ws) all.push_back(e.part_ws);
+    for (Workspace* w : all) free_workspace(w);
+    e.ws_pool.clear();
+    e.part_ws = nullptr;
   }
   if (e.free_stream) {  // device_init makes a new one for the next snapshot
     (void)hipSetDevice(e.device);
@@ -1336,12 +1381,23 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     delete e.dev;
   }
   e.dev = ds;
-  e.generation++;
+  static std::atomic<uint64_t> g_generations{0};  // process-wide: a snapshot id never repeats
+  e.generation = ++g_generations;
   HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
 }
 
-static Workspace* ensure_workspace(Engine& e) {
-  if (e.ws) return e.ws;
+// ---- workspaces ------------------------------------------------------------------------------
+
+static uint32_t device_cus(int device) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    return (uint32_t)prop.multiProcessorCount;
+  return 256;
+}
+
+// A workspace with its counters, staging and bundle scratch; the grid-wide and workgroup-bundle
+// scratch follow on first use (ensure_wide / ensure_giant), since most batches never need them.
+static Workspace* create_workspace(Engine& e) {
   HIP_OK(hipSetDevice(e.device));
   auto* w = new Workspace();
   try {
@@ -1357,14 +1413,6 @@ static Workspace* ensure_workspace(Engine& e) {
     w->query_cap = std::max(w->query_cap, w->max_batch);
     if (w->frontier_cap > 0xFFFFFFF0ull || w->query_cap > 0x7FFFFFFFull)
       throw Error(GCK_E_INVALID_ARGUMENT, "workspace capacity too large");
-    w->checks = dalloc<DevCheck>(w->allocs, w->max_batch);
-    w->item_err = dalloc<int32_t>(w->allocs, w->max_batch);
-    w->queries = dalloc<DevQuery>(w->allocs, w->query_cap);
-    w->joins = dalloc<DevJoin>(w->allocs, w->join_cap);
-    w->fr[0] = dalloc<Entry>(w->allocs, w->frontier_cap);
-    w->fr[1] = dalloc<Entry>(w->allocs, w->frontier_cap);
-    w->segs = dalloc<Segment>(w->allocs, w->seg_cap);
-    w->visited = dalloc<unsigned long long>(w->allocs, w->visited_cap);
     // the level / batch counters and the bundle counters share one buffer (one memset, one copy
     // back per batch)
     static_assert(sizeof(DevCounters) % 8 == 0, "bundle counters follow DevCounters");
@@ -1379,12 +1427,16 @@ static Workspace* ensure_workspace(Engine& e) {
     w->h_seq = w->h_bctrs + 4;
     *w->h_seq = 0;
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&w->d_hpub), w->h_ctr, 0));
+    // pinned staging of host batches: 20 B of items in, 5 B of results out per check
+    const size_t stage = w->max_batch * (sizeof(gck_item) + 1 + 4);
+    void* hs = nullptr;
+    HIP_OK(hipHostMalloc(&hs, stage, hipHostMallocDefault));
+    w->h_items = static_cast<gck_item*>(hs);
+    w->h_err = reinterpret_cast<int32_t*>(w->h_items + w->max_batch);
+    w->h_perm = reinterpret_cast<uint8_t*>(w->h_err + w->max_batch);
     // bundle path scratch: per resident wavefront, a frontier pair and a visited table
     if (!(cf.flags & GCK_FLAG_NO_BUNDLE)) {
-      int cus = 256;
-      hipDeviceProp_t prop;
-      if (hipGetDeviceProperties(&prop, e.device) == hipSuccess && prop.multiProcessorCount > 0)
-        cus = prop.multiProcessorCount;
+      const uint32_t cus = device_cus(e.device);
       // 8 resident bundle waves per CU with 32 checks each: the level latency of this gather-bound
       // loop grows with the requests in flight, so fewer, fuller waves finish a batch sooner
       // (config 4 sweep, profiles/r01/sweeps: 16 x 16 -> 250 M/s, 8 x 32 -> 323 M/s)
@@ -1392,26 +1444,24 @@ static Workspace* ensure_workspace(Engine& e) {
       w->b_checks = cf.bundle_checks ? std::min<uint32_t>(cf.bundle_checks, kBMax) : 32;
       w->b_fc = cf.bundle_frontier ? cf.bundle_frontier : 4096;
       w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 16384);
-      w->b_blocks = std::max<uint32_t>(1, (uint32_t)cus * wpc / kWaves);
+      w->b_blocks = std::max<uint32_t>(1, cus * wpc / kWaves);
       const size_t slots = (size_t)w->b_blocks * kWaves;
       w->b_fr = dalloc<unsigned long long>(w->allocs, slots * 2 * w->b_fc);
       w->b_vis = dalloc<unsigned long long>(w->allocs, slots * w->b_vslots);
       w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots);
-      HIP_OK(hipMemset(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long)));
+      HIP_OK(hipMemsetAsync(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long), nullptr));
       w->b_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
       w->b_budget = cf.bundle_budget ? cf.bundle_budget : 1024;
       w->g_fc = cf.giant_frontier ? cf.giant_frontier : 65536;
       w->g_vslots = 1u << ceil_log2(cf.giant_visited ? cf.giant_visited : 262144);
-      w->g_slots = cf.giant_slots ? cf.giant_slots : (uint32_t)cus;
-      w->g_fr = dalloc<unsigned long long>(w->allocs, (size_t)w->g_slots * 2 * w->g_fc);
-      w->g_vis = dalloc<unsigned long long>(w->allocs, (size_t)w->g_slots * w->g_vslots);
-      w->g_vlog = dalloc<uint32_t>(w->allocs, (size_t)w->g_slots * w->g_vslots);
-      HIP_OK(hipMemset(w->g_vis, 0, (size_t)w->g_slots * w->g_vslots * sizeof(unsigned long long)));
+      w->g_slots = cf.giant_slots ? cf.giant_slots : cus;
       w->g_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
       w->def_items = dalloc<gck_item>(w->allocs, w->max_batch);
       w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
       w->def_err = dalloc<int32_t>(w->allocs, w->max_batch);
     }
+    HIP_OK(hipMemsetAsync(w->ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), nullptr));
+    w->ctr_clean = true;
     HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&w->ev0));
     HIP_OK(hipEventCreate(&w->ev1));
@@ -1419,18 +1469,68 @@ static Workspace* ensure_workspace(Engine& e) {
     for (hipEvent_t& ev : w->pev) HIP_OK(hipEventCreate(&ev));
     HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
   } catch (...) {
-    free_list(w->allocs);
-    if (w->h_ctr) (void)hipHostFree(w->h_ctr);
-    delete w;
+    free_workspace(w);
     throw;
   }
-  e.ws = w;
   return w;
 }
 
-static bool next_pow2_fits(uint32_t bits_q, size_t query_cap) { return (1ull << bits_q) >= query_cap; }
+// The grid-wide path's scratch (stage C, lookups' giant candidates, partitioned batches).
+static void ensure_wide(Workspace& w) {
+  if (w.wide_ready) return;
+  w.checks = dalloc<DevCheck>(w.allocs, w.max_batch);
+  w.item_err = dalloc<int32_t>(w.allocs, w.max_batch);
+  w.queries = dalloc<DevQuery>(w.allocs, w.query_cap);
+  w.joins = dalloc<DevJoin>(w.allocs, w.join_cap);
+  w.fr[0] = dalloc<Entry>(w.allocs, w.frontier_cap);
+  w.fr[1] = dalloc<Entry>(w.allocs, w.frontier_cap);
+  w.segs = dalloc<Segment>(w.allocs, w.seg_cap);
+  w.visited = dalloc<unsigned long long>(w.allocs, w.visited_cap);
+  HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
+  w.wide_ready = true;
+}
 
-// Runs one batch (n <= max_batch). Returns false on a workspace overflow (caller splits).
+// The workgroup-bundle stage's scratch (stage B).
+static void ensure_giant(Workspace& w) {
+  if (w.giant_ready) return;
+  w.g_fr = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * 2 * w.g_fc);
+  w.g_vis = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * w.g_vslots);
+  w.g_vlog = dalloc<uint32_t>(w.allocs, (size_t)w.g_slots * w.g_vslots);
+  HIP_OK(hipMemsetAsync(w.g_vis, 0, (size_t)w.g_slots * w.g_vslots * sizeof(unsigned long long), nullptr));
+  HIP_OK(hipStreamSynchronize(nullptr));
+  w.giant_ready = true;
+}
+
+// A free workspace of the pool (created while the pool holds fewer than cfg.workspaces;
+// otherwise waits for one to be released). Call without holding the engine lock: the holders of
+// busy workspaces may need it to finish their batches.
+Workspace* acquire_ws(Engine& e) {
+  const size_t cap = e.cfg.workspaces ? e.cfg.workspaces : 4;
+  std::unique_lock<std::mutex> lk(e.ws_mu);
+  for (;;) {
+    for (Workspace* w : e.ws_pool)
+      if (!w->busy) {
+        w->busy = true;
+        return w;
+      }
+    if (e.ws_pool.size() < cap) {
+      Workspace* w = create_workspace(e);
+      w->busy = true;
+      e.ws_pool.push_back(w);
+      return w;
+    }
+    e.ws_cv.wait(lk);
+  }
+}
+
+void release_ws(Engine& e, Workspace* w) {
+  {
+    std::lock_guard<std::mutex> lk(e.ws_mu);
+    w->busy = false;
+  }
+  e.ws_cv.notify_one();
+}
+
 static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   DeviceSnapshot& ds = *e.dev;
   Ctx c{};
@@ -1454,8 +1554,7 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.frontier_cap = (uint32_t)w.frontier_cap;
   c.seg_cap = (uint32_t)std::min<size_t>(w.seg_cap, (1u << 24) - 1);
   const uint32_t q_bits = ds.any_deep ? ds.q_bits_deep : ds.q_bits;
-  uint32_t qcap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << q_bits);
-  c.query_cap = qcap;
+  c.query_cap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << q_bits);
   c.join_cap = (uint32_t)w.join_cap;
   c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
   if (ds.any_deep) {  // exact-depth checks key their entries by depth (make_key)
@@ -1475,17 +1574,29 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.cav_row = ds.cav_row;
   c.cav_dyn = w.cav_dyn;
   c.n_ctx = w.cav_dyn ? w.n_ctx : 0u;
-  (void)next_pow2_fits;
   return c;
 }
 
+static void add_counters(Engine& e, const DevCounters& h) {
+  std::lock_guard<std::mutex> lk(e.stats_mu);
+  e.stats.entries_expanded += h.expanded;
+  e.stats.row_lookups += h.row_lookups;
+  e.stats.membership_probes += h.probes;
+  e.stats.edges_enumerated += h.edges;
+  e.stats.ext_edges += h.ext_edges;
+  e.stats.bidir_checks += h.bidir;
+}
+
+// Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
+// (the caller splits the batch).
 static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                       uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
+  ensure_wide(w);
   Ctx c = make_ctx(e, w, now_us);
   c.ck_items = d_items;
   HIP_OK(hipEventRecord(w.ev0, st));
   w.ctr_clean = false;
-  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters), st));
+  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));
   HIP_OK(hipMemsetAsync(w.visited, 0xFF, w.visited_cap * sizeof(unsigned long long), st));
   DevCounters init{};
   init.n_queries = n;
@@ -1499,14 +1610,13 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   uint32_t n_cur = n;
   int cur = 0;
   const uint32_t level_cap = 64 * c.max_depth + 64;
-  float expand_ms = 0.f;
+  uint64_t levels = 0;
   for (uint32_t level = 0; n_cur > 0; ++level) {
     if (level > level_cap) throw Error(GCK_E_DEVICE, "level cap exceeded (engine invariant)");
     c.level = level;
     c.next = w.fr[cur ^ 1];
     if (profile) HIP_OK(hipEventRecord(w.pev[0], st));
-    hipLaunchKernelGGL(k_expand, dim3((n_cur + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c,
-                       w.fr[cur], n_cur);
+    hipLaunchKernelGGL(k_expand, dim3((n_cur + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c, w.fr[cur], n_cur);
     if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
     hipLaunchKernelGGL(k_edges, dim3(2048), dim3(kBlock), 0, st, c);
     if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
@@ -1521,6 +1631,7 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
       HIP_OK(hipEventElapsedTime(&a, w.pev[0], w.pev[1]));
       HIP_OK(hipEventElapsedTime(&b, w.pev[1], w.pev[2]));
       HIP_OK(hipEventElapsedTime(&r, w.pev[2], w.pev[3]));
+      std::lock_guard<std::mutex> lk(e.stats_mu);
       e.stats.expand_ms += a;
       e.stats.edges_ms += b;
       e.stats.resolve_ms += r;
@@ -1530,10 +1641,9 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
     if (w.h_ctr->overflow) return false;
     n_cur = w.h_ctr->last_next;
     cur ^= 1;
-    e.stats.levels++;
+    ++levels;
   }
-  hipLaunchKernelGGL(k_final, dim3(grid_n), dim3(kBlock), 0, st, w.queries, n, w.item_err, d_perm,
-                     d_err, w.ctr);
+  hipLaunchKernelGGL(k_final, dim3(grid_n), dim3(kBlock), 0, st, w.queries, n, w.item_err, d_perm, d_err, w.ctr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(w.ev1, st));
   HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
@@ -1543,13 +1653,10 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, w.ev0, w.ev1));
   *ms_out += ms;
-  (void)expand_ms;
   const DevCounters& h = *w.h_ctr;
-  e.stats.entries_expanded += h.expanded;
-  e.stats.row_lookups += h.row_lookups;
-  e.stats.membership_probes += h.probes;
-  e.stats.edges_enumerated += h.edges;
-  e.stats.ext_edges += h.ext_edges;
+  add_counters(e, h);
+  std::lock_guard<std::mutex> lk(e.stats_mu);
+  e.stats.levels += levels;
   e.stats.queries += h.n_queries;
   e.stats.joins += h.n_joins;
   e.stats.batches++;
@@ -1562,7 +1669,10 @@ static void check_range_wide(Engine& e, Workspace& w, const gck_item* d_items, s
   while (pos < n) {
     size_t len = std::min(n - pos, w.max_batch);
     while (!run_batch(e, w, d_items + pos, (uint32_t)len, now_us, d_perm + pos, d_err + pos, st, ms)) {
-      e.stats.retries++;
+      {
+        std::lock_guard<std::mutex> lk(e.stats_mu);
+        e.stats.retries++;
+      }
       if (len == 1) throw Error(GCK_E_CAPACITY, "device workspace overflow on a single check");
       len = (len + 1) / 2;
     }
@@ -1591,13 +1701,29 @@ static void wait_published(Workspace& w, hipStream_t st, unsigned seq) {
   }
 }
 
-// One persistent bundle launch over n <= max_batch checks, then the grid-wide path for the
-// checks whose bundle overflowed its per-wave scratch.
-static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
-                        uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
-  Ctx c = make_ctx(e, w, now_us);
-  c.ck_items = d_items;
-  const bool profile = (e.cfg.flags & GCK_FLAG_PROFILE) != 0;
+// elapsed time of a published batch: its events are complete, though the runtime may not have
+// marked them yet (synchronise only then)
+static void elapsed_ms(float* out, hipEvent_t a, hipEvent_t b) {
+  hipError_t r = hipEventElapsedTime(out, a, b);
+  if (r == hipErrorNotReady) {
+    HIP_OK(hipEventSynchronize(b));
+    r = hipEventElapsedTime(out, a, b);
+  }
+  HIP_OK(r);
+}
+
+constexpr uint32_t kPubWords = (sizeof(DevCounters) + 4 * sizeof(unsigned)) / 4;
+
+static void publish_launch(Workspace& w, hipStream_t st) {
+  const unsigned seq = ++w.pub_seq;
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, reinterpret_cast<unsigned*>(w.ctr), kPubWords, w.d_hpub,
+                     w.d_hpub + kPubWords, seq);
+  HIP_OK(hipGetLastError());
+  w.b_seq = seq;
+}
+
+static BundleArgs bundle_args(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, uint8_t* d_perm,
+                              int32_t* d_err) {
   BundleArgs a{};
   a.items = d_items;
   a.n = n;
@@ -1613,67 +1739,48 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   a.vis_base = w.b_vis;
   a.vlog_base = w.b_vlog;
   static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
-  static uint32_t* dbg = nullptr;
-  const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;
-  if (dbg_on && !dbg) HIP_OK(hipMalloc(&dbg, dbg_words * 4));
-  a.dbg = dbg_on ? dbg : nullptr;
+  if (dbg_on && !w.dbg) HIP_OK(hipMalloc(&w.dbg, (4 + kBQ * 6 + kBJ * 8) * 4));
+  a.dbg = dbg_on ? w.dbg : nullptr;
   a.budget = w.b_budget;
   a.both = e.cfg.bidir_both ? e.cfg.bidir_both : 64;
   a.idx = nullptr;
   a.n_dev = nullptr;
   // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
-  static unsigned long long* timing = nullptr;
   const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
-  static size_t timing_cap = 0;
-  if (timing_env && timing_cap < timing_words) {
-    if (timing) (void)hipFree(timing);
-    HIP_OK(hipMalloc(&timing, timing_words * 8));
-    timing_cap = timing_words;
+  if (timing_env && w.timing_cap < timing_words) {
+    if (w.timing) (void)hipFree(w.timing);
+    w.timing = nullptr;
+    HIP_OK(hipMalloc(&w.timing, timing_words * 8));
+    w.timing_cap = timing_words;
   }
-  a.timing = timing_env ? timing : nullptr;
-  // stage B: giant checks, one 16-wave workgroup each, over stage A's deferred list (its length
-  // is read on the device, so both stages are queued back to back without a host round trip)
-  BundleArgs g = a;
-  g.idx = w.b_deferred;
-  g.n = n;
-  g.n_dev = w.b_ctrs + 1;
-  g.deferred = w.g_deferred;
-  g.n_deferred = w.b_ctrs + 3;
-  g.bundle_ctr = w.b_ctrs + 2;
-  g.B = 1;
-  g.FC = w.g_fc;
-  g.vmask = w.g_vslots - 1;
-  g.budget = 0xFFFFFFFFu;
-  g.fr_base = w.g_fr;
-  g.vis_base = w.g_vis;
-  g.vlog_base = w.g_vlog;
-  g.dbg = nullptr;
-  g.timing = timing_env ? timing + (size_t)kTimingWords * (n + 1) : nullptr;
-  if (timing_env) HIP_OK(hipMemsetAsync(timing, 0, timing_words * 8, st));
-  static const bool stream_sync = getenv("GCK_SYNC_STREAM") != nullptr;  // A/B: copy + stream sync
-  if (!w.ctr_clean || stream_sync)
-    HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));  // + b_ctrs
-  w.ctr_clean = false;
-  // one event opens the batch and, with profiling, stage A (pev[0] aliases ev0); one closes
-  // stage A and, with nothing deferred, the batch (ev1 aliases pev[1]): every record is a
-  // host API call on the per-batch path
-  HIP_OK(hipEventRecord(w.ev0, st));
-  hipEvent_t ev_end = w.ev1;
-  // events of a published batch are complete, though the runtime may not have marked them
-  // yet: synchronise only then
-  auto elapsed = [](float* out, hipEvent_t a, hipEvent_t b) {
-    hipError_t r = hipEventElapsedTime(out, a, b);
-    if (r == hipErrorNotReady) {
-      HIP_OK(hipEventSynchronize(b));
-      r = hipEventElapsedTime(out, a, b);
-    }
-    HIP_OK(r);
-  };
-  // the node program is staged in LDS when it fits (bundle.inc)
+  a.timing = timing_env ? w.timing : nullptr;
+  return a;
+}
+
+// The node program is staged in LDS when it fits (bundle.inc).
+static bool program_in_lds(const Ctx& c) {
   const size_t prog_bytes = (size_t)c.n_csrs * sizeof(DevCSR) + (size_t)c.n_nodes * sizeof(DevNode) +
                             (size_t)c.n_items * sizeof(DevItem);
-  const bool prog_lds = prog_bytes <= (size_t)kProgBytes;
+  return prog_bytes <= (size_t)kProgBytes;
+}
+
+// Stage A of a bundle batch (n <= max_batch): the persistent wave-bundle kernel over every
+// check, then — for a host batch — the copy of the results into the pinned staging, and the
+// publication the host spins on. Nothing waits here.
+static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
+                           uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
+  Ctx c = make_ctx(e, w, now_us);
+  c.ck_items = d_items;
+  BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
+  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  if (timing_env) HIP_OK(hipMemsetAsync(w.timing, 0, w.timing_cap * 8, st));
+  if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));  // + b_ctrs
+  w.ctr_clean = false;
+  // one event opens the batch and stage A, one closes stage A: every record is a host API call
+  // on the per-batch path
+  HIP_OK(hipEventRecord(w.ev0, st));
+  const bool prog_lds = program_in_lds(c);
   // bidirectional instantiation only when the snapshot has an eligible permission (bidir.inc)
   const bool bd = e.dev->has_bidir;
   if (prog_lds && bd)
@@ -1685,83 +1792,117 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
   else
     hipLaunchKernelGGL((k_bundles<1, kLFWave, false, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
   HIP_OK(hipGetLastError());
-  if (profile) HIP_OK(hipEventRecord(w.pev[1], st));
+  HIP_OK(hipEventRecord(w.ev1, st));
+  if (host_out) {
+    HIP_OK(hipMemcpyAsync(w.h_perm, d_perm, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.h_err, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  }
+  publish_launch(w, st);
+}
+
+static void debug_dump(Engine& e, Workspace& w, uint32_t n);
+
+// Stages B and C of a bundle batch after stage A was published: the checks stage A deferred
+// (giant, or rooted high enough to need exact depth) through the workgroup bundles and/or the
+// grid-wide path, synchronously. Returns the device time of the batch.
+static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
+                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
+  wait_published(w, st, w.b_seq);
+  add_counters(e, *w.h_ctr);
+  w.ctr_clean = true;  // k_publish zeroed the device counters
+  const bool profile = (e.cfg.flags & GCK_FLAG_PROFILE) != 0;
+  float ms = 0.f, bm = 0.f, gm = 0.f;
+  elapsed_ms(&ms, w.ev0, w.ev1);
+  bm = ms;
+  const uint32_t n_def = w.h_bctrs[1];
+  uint32_t n_def2 = n_def;
   const bool giant = !(e.cfg.flags & GCK_FLAG_NO_GIANT);
-  auto launch_giant = [&] {
-    if (prog_lds)
+  if (n_def > n) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
+  if (n_def > 0 && giant) {
+    // stage B: giant checks, one 16-wave workgroup each, over stage A's deferred list (the
+    // publish zeroed the deferred count on the device: restore it first)
+    ensure_giant(w);
+    Ctx c = make_ctx(e, w, now_us);
+    c.ck_items = d_items;
+    BundleArgs g = bundle_args(e, w, d_items, n, d_perm, d_err);
+    g.idx = w.b_deferred;
+    g.n_dev = w.b_ctrs + 1;
+    g.deferred = w.g_deferred;
+    g.n_deferred = w.b_ctrs + 3;
+    g.bundle_ctr = w.b_ctrs + 2;
+    g.B = 1;
+    g.FC = w.g_fc;
+    g.vmask = w.g_vslots - 1;
+    g.budget = 0xFFFFFFFFu;
+    g.fr_base = w.g_fr;
+    g.vis_base = w.g_vis;
+    g.vlog_base = w.g_vlog;
+    g.dbg = nullptr;
+    g.timing = g.timing ? g.timing + (size_t)kTimingWords * (n + 1) : nullptr;
+    w.h_seq[1] = n_def;
+    HIP_OK(hipMemcpyAsync(w.b_ctrs + 1, w.h_seq + 1, sizeof(unsigned), hipMemcpyHostToDevice, st));
+    w.ctr_clean = false;
+    HIP_OK(hipEventRecord(w.ev0, st));
+    if (program_in_lds(c))
       hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, true, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
     else
       hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, false, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
     HIP_OK(hipGetLastError());
-  };
-  auto add_counters = [&] {
-    const DevCounters& h = *w.h_ctr;
-    e.stats.entries_expanded += h.expanded;
-    e.stats.row_lookups += h.row_lookups;
-    e.stats.membership_probes += h.probes;
-    e.stats.edges_enumerated += h.edges;
-    e.stats.ext_edges += h.ext_edges;
-    e.stats.bidir_checks += h.bidir;
-  };
-  constexpr uint32_t n_words = (sizeof(DevCounters) + 4 * sizeof(unsigned)) / 4;
-  auto publish = [&] {
-    const unsigned seq = ++w.pub_seq;
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, reinterpret_cast<unsigned*>(w.ctr), n_words, w.d_hpub,
-                       w.d_hpub + n_words, seq);
-    HIP_OK(hipGetLastError());
-    wait_published(w, st, seq);
-    add_counters();
-  };
-  float gm = 0.f;
-  uint32_t n_def = 0, n_def2 = 0;
-  if (stream_sync) {  // both stages queued back to back, stage B reads the deferred count on the device
-    if (giant) launch_giant();
-    if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
-    HIP_OK(hipMemcpyAsync(w.h_ctr, w.ctr, n_words * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipEventRecord(w.ev1, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (profile) HIP_OK(hipEventElapsedTime(&gm, w.pev[1], w.pev[2]));
-    add_counters();
-    n_def = w.h_bctrs[1];
-    n_def2 = giant ? w.h_bctrs[3] : n_def;
-  } else {
-    // stage A is published first; stage B is launched only when it deferred a check (none do
-    // on the benchmark configs), after restoring the deferred count the publish zeroed
-    if (profile) ev_end = w.pev[1];
-    else HIP_OK(hipEventRecord(w.ev1, st));
-    publish();
-    n_def = n_def2 = w.h_bctrs[1];
-    if (giant && n_def > 0 && n_def <= n) {
-      w.h_seq[1] = n_def;
-      HIP_OK(hipMemcpyAsync(w.b_ctrs + 1, w.h_seq + 1, sizeof(unsigned), hipMemcpyHostToDevice, st));
-      if (profile) HIP_OK(hipEventRecord(w.pev[3], st));
-      launch_giant();
-      if (profile) HIP_OK(hipEventRecord(w.pev[2], st));
-      HIP_OK(hipEventRecord(w.ev1, st));
-      ev_end = w.ev1;
-      publish();
-      if (profile) elapsed(&gm, w.pev[3], w.pev[2]);
-      n_def2 = w.h_bctrs[3];
-    }
+    publish_launch(w, st);
+    wait_published(w, st, w.b_seq);
+    add_counters(e, *w.h_ctr);
     w.ctr_clean = true;
+    elapsed_ms(&gm, w.ev0, w.ev1);
+    ms += gm;
+    n_def2 = w.h_bctrs[3];
+    if (n_def2 > n_def) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
   }
-  float ms = 0.f;
-  elapsed(&ms, w.ev0, stream_sync ? w.ev1 : ev_end);
-  *ms_out += ms;
-  if (profile) {
-    float b = 0.f;
-    elapsed(&b, w.ev0, w.pev[1]);
-    e.stats.bundle_ms += b;
-    e.stats.giant_ms += gm;
-    e.stats.bundle_launches++;
+  debug_dump(e, w, n);
+  {
+    std::lock_guard<std::mutex> lk(e.stats_mu);
+    if (profile) {
+      e.stats.bundle_ms += bm;
+      e.stats.giant_ms += gm;
+      e.stats.bundle_launches++;
+    }
+    e.stats.queries += n;
+    e.stats.batches++;
+    e.stats.deferred += n_def;
+    e.stats.deferred_wide += n_def2;
   }
-  e.stats.queries += n;
-  e.stats.batches++;
-  if (dbg_on) {
+  if (n_def == 0) return ms;
+  if (n_def2 > 0) {
+    // stage C: the grid-wide level-synchronous path for what outgrew a workgroup bundle or
+    // needs exact depth
+    const uint32_t* def_idx = giant ? w.g_deferred : w.b_deferred;
+    const uint32_t grid = (n_def2 + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, def_idx, n_def2, w.def_items);
+    HIP_OK(hipGetLastError());
+    check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, &ms);
+    hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, def_idx, n_def2, w.def_perm, w.def_err, d_perm,
+                       d_err);
+    HIP_OK(hipGetLastError());
+  }
+  if (host_out) {  // the deferred checks' results, in place in the staging
+    HIP_OK(hipMemcpyAsync(w.h_perm, d_perm, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.h_err, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  return ms;
+}
+
+// GCK_DEBUG_BUNDLE: bundle 0's final query / join tables; GCK_DEBUG_TIMING: both stages'
+// per-bundle records appended to <prefix>.bin (kTimingWords u64 each).
+static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
+  static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
+  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  if (dbg_on && w.dbg) {
+    const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;
     std::vector<uint32_t> h(dbg_words);
-    HIP_OK(hipMemcpy(h.data(), dbg, dbg_words * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(h.data(), w.dbg, dbg_words * 4, hipMemcpyDeviceToHost));
     fprintf(stderr, "[gck bundle0] queries=%u joins=%u overflow=%u epoch=%u\n", h[0], h[1], h[2], h[3]);
     for (uint32_t k = 0; k < h[0] && k < (uint32_t)kBQ; ++k) {
       const uint32_t* d = h.data() + 4 + k * 6;
@@ -1770,13 +1911,14 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
     }
     for (uint32_t k = 0; k < h[1] && k < (uint32_t)kBJ; ++k) {
       const uint32_t* d = h.data() + 4 + kBQ * 6 + k * 8;
-      fprintf(stderr, "  j%-3u parent=%u first=%u n=%u op=%u cond=%u state=%#x remaining=%d\n", k, d[0], d[1],
-              d[2], d[3], d[4], d[5], (int)d[6]);
+      fprintf(stderr, "  j%-3u parent=%u first=%u n=%u op=%u cond=%u state=%#x remaining=%d\n", k, d[0], d[1], d[2],
+              d[3], d[4], d[5], (int)d[6]);
     }
   }
-  if (timing_env) {  // append both stages' per-bundle records to <prefix>.bin (kTimingWords u64 each)
+  if (timing_env && w.timing) {
+    const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
     std::vector<unsigned long long> h(timing_words);
-    HIP_OK(hipMemcpy(h.data(), timing, timing_words * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(h.data(), w.timing, timing_words * 8, hipMemcpyDeviceToHost));
     std::string path = std::string(timing_env) + ".bin";
     if (FILE* f = fopen(path.c_str(), "ab")) {
       unsigned long long hdr[4] = {0xB0DDull, n, w.b_checks, w.h_bctrs[1]};
@@ -1785,32 +1927,7 @@ static void run_bundles(Engine& e, Workspace& w, const gck_item* d_items, uint32
       fclose(f);
     }
   }
-  const uint32_t* def_idx = giant ? w.g_deferred : w.b_deferred;
-  if (n_def > n || n_def2 > n_def) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");
-  e.stats.deferred += n_def;
-  e.stats.deferred_wide += n_def2;
-  if (n_def2 == 0) return;
-  // stage C: the grid-wide level-synchronous path for what outgrew a workgroup bundle
-  const uint32_t grid = (n_def2 + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, def_idx, n_def2, w.def_items);
-  HIP_OK(hipGetLastError());
-  check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, ms_out);
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, def_idx, n_def2, w.def_perm, w.def_err,
-                     d_perm, d_err);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipStreamSynchronize(st));
-}
-
-static void check_range(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us,
-                        uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms) {
-  if (e.cfg.flags & GCK_FLAG_NO_BUNDLE) {
-    check_range_wide(e, w, d_items, n, now_us, d_perm, d_err, st, ms);
-    return;
-  }
-  for (size_t pos = 0; pos < n; pos += w.max_batch) {
-    const uint32_t len = (uint32_t)std::min(n - pos, w.max_batch);
-    run_bundles(e, w, d_items + pos, len, now_us, d_perm + pos, d_err + pos, st, ms);
-  }
+  (void)e;
 }
 
 static int64_t wall_now_us() {
@@ -1833,43 +1950,190 @@ static void stage_caveats(Workspace& w, const std::vector<uint8_t>& table, uint3
     w.cav_dyn = dalloc<uint8_t>(w.allocs, w.cav_dyn_cap);
     HIP_OK(hipStreamSynchronize(nullptr));  // the allocation is ordered on the null stream
   }
+  // pageable source: the copy has completed when the call returns, so the table may go
   HIP_OK(hipMemcpyAsync(w.cav_dyn, table.data(), table.size(), hipMemcpyHostToDevice, st));
+  HIP_OK(hipStreamSynchronize(st));
 }
 
-void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
+// ---- batches ---------------------------------------------------------------------------------
+//
+// A batch is started by submit_batch (everything is queued, nothing waited for) and completed by
+// finish_batch (stage A waited for, the later stages run, a host batch's results copied out of
+// the pinned staging). The synchronous entry points are the two back to back; gck_check_submit /
+// gck_check_wait expose them separately so that the next batch is queued while this one runs.
+
+static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_t n, int64_t now_us, uint8_t* perm,
+                         int32_t* err, hipStream_t st, bool host) {
+  w.b_n = n;
+  w.b_now = now_us;
+  w.b_st = host ? w.stream : st;
+  w.b_hperm = host ? perm : nullptr;
+  w.b_herr = host ? err : nullptr;
+  w.b_items = host ? w.d_items : items;
+  w.b_dperm = host ? w.d_perm : perm;
+  w.b_derr = host ? w.d_err : err;
+  w.b_ms = 0.f;
+  w.fail_code = 0;
+  w.fail_msg.clear();
+  if (host) {
+    // the caller's (pageable) items through the pinned staging: one host copy, one DMA
+    std::memcpy(w.h_items, items, (size_t)n * sizeof(gck_item));
+    HIP_OK(hipMemcpyAsync(w.d_items, w.h_items, (size_t)n * sizeof(gck_item), hipMemcpyHostToDevice, w.b_st));
+  }
+  if (e.cfg.flags & GCK_FLAG_NO_BUNDLE) {
+    w.b_bundles = false;
+  } else {
+    w.b_bundles = true;
+    bundles_launch(e, w, w.b_items, n, now_us, w.b_dperm, w.b_derr, w.b_st, host);
+  }
+  w.state = 1;
+}
+
+// Completes the batch in flight (caller holds w.m). The results are in the caller's device
+// buffers, or in the pinned staging for a host batch.
+static void finish_batch(Engine& e, Workspace& w) {
+  if (w.state != 1) return;
+  w.state = 2;
+  if (w.b_bundles) {
+    w.b_ms = bundles_finish(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, w.b_hperm != nullptr);
+  } else {
+    check_range_wide(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, &w.b_ms);
+    if (w.b_hperm) {
+      HIP_OK(hipMemcpyAsync(w.h_perm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, w.b_st));
+      HIP_OK(hipMemcpyAsync(w.h_err, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, w.b_st));
+      HIP_OK(hipStreamSynchronize(w.b_st));
+    }
+  }
+}
+
+static void copy_out(Workspace& w) {
+  if (!w.b_hperm) return;
+  std::memcpy(w.b_hperm, w.h_perm, w.b_n);
+  std::memcpy(w.b_herr, w.h_err, (size_t)w.b_n * 4);
+}
+
+void drain_batches(Engine& e) {
+  std::vector<Workspace*> busy;
+  {
+    std::lock_guard<std::mutex> lk(e.ws_mu);
+    for (Workspace* w : e.ws_pool)
+      if (w->busy) busy.push_back(w);
+  }
+  for (Workspace* w : busy) {
+    std::lock_guard<std::mutex> lk(w->m);
+    if (w->state != 1) continue;
+    try {
+      finish_batch(e, *w);
+    } catch (const Error& ex) {
+      w->fail_code = ex.code;
+      w->fail_msg = ex.what();
+    }
+  }
+}
+
+void device_check(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
                   int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
   HIP_OK(hipSetDevice(e.device));
-  std::lock_guard<std::mutex> lk(e.ws_mu);
-  Workspace& w = *ensure_workspace(e);
-  // the caller's stream; NULL is the legacy default stream (never the engine's own non-blocking
-  // stream, which would not be ordered after the caller's writes of the items and outputs)
+  std::lock_guard<std::mutex> lk(w.m);
+  // the caller's stream; NULL is the legacy default stream (never the workspace's own
+  // non-blocking stream, which would not be ordered after the caller's writes of the items)
   hipStream_t st = (hipStream_t)stream;
   stage_caveats(w, cav_table, n_ctx, st);
   if (now_us == 0) now_us = wall_now_us();
   float ms = 0.f;
-  check_range(e, w, d_items, n, now_us, d_perm, d_err, st, &ms);
+  for (size_t pos = 0; pos < n; pos += w.max_batch) {
+    const uint32_t len = (uint32_t)std::min(n - pos, w.max_batch);
+    submit_batch(e, w, d_items + pos, len, now_us, d_perm + pos, d_err + pos, st, false);
+    finish_batch(e, w);
+    w.state = 0;
+    ms += w.b_ms;
+  }
+  std::lock_guard<std::mutex> sl(e.stats_mu);
   e.stats.kernel_ms = ms;
 }
 
-void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                       int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
+// Host buffers: chunks of max_batch on two workspaces in turn, so that a chunk's copies and
+// host staging overlap the previous chunk's kernels.
+void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* items, size_t n, int64_t now_us,
+                       uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
   HIP_OK(hipSetDevice(e.device));
-  std::lock_guard<std::mutex> lk(e.ws_mu);
-  Workspace& w = *ensure_workspace(e);
-  stage_caveats(w, cav_table, n_ctx, w.stream);
   if (now_us == 0) now_us = wall_now_us();
+  const size_t mb = w0->max_batch;
+  const size_t n_chunks = (n + mb - 1) / mb;
+  Workspace* ws[2] = {w0, (w1 && n_chunks > 1) ? w1 : w0};
+  std::lock_guard<std::mutex> g0(ws[0]->m);
+  std::unique_ptr<std::lock_guard<std::mutex>> g1;
+  if (ws[1] != ws[0]) g1.reset(new std::lock_guard<std::mutex>(ws[1]->m));
+  for (Workspace* w : {ws[0], ws[1]}) stage_caveats(*w, cav_table, n_ctx, w->stream);
   float ms = 0.f;
-  size_t pos = 0;
-  while (pos < n) {
-    size_t len = std::min(n - pos, w.max_batch);
-    HIP_OK(hipMemcpyAsync(w.d_items, items + pos, len * sizeof(gck_item), hipMemcpyHostToDevice, w.stream));
-    check_range(e, w, w.d_items, len, now_us, w.d_perm, w.d_err, w.stream, &ms);
-    HIP_OK(hipMemcpyAsync(perm + pos, w.d_perm, len, hipMemcpyDeviceToHost, w.stream));
-    HIP_OK(hipMemcpyAsync(err + pos, w.d_err, len * 4, hipMemcpyDeviceToHost, w.stream));
-    HIP_OK(hipStreamSynchronize(w.stream));
-    pos += len;
+  Workspace* prev = nullptr;
+  for (size_t k = 0; k < n_chunks; ++k) {
+    Workspace& w = *ws[k & 1];
+    const size_t pos = k * mb;
+    const uint32_t len = (uint32_t)std::min(n - pos, mb);
+    submit_batch(e, w, items + pos, len, now_us, perm + pos, err + pos, nullptr, true);
+    if (prev) {
+      finish_batch(e, *prev);
+      copy_out(*prev);
+      prev->state = 0;
+      ms += prev->b_ms;
+    }
+    prev = &w;
   }
+  if (prev) {
+    finish_batch(e, *prev);
+    copy_out(*prev);
+    prev->state = 0;
+    ms += prev->b_ms;
+  }
+  std::lock_guard<std::mutex> sl(e.stats_mu);
   e.stats.kernel_ms = ms;
+}
+
+void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
+                   int32_t* err, void* stream, bool host, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
+  HIP_OK(hipSetDevice(e.device));
+  std::lock_guard<std::mutex> lk(w->m);
+  if (n > w->max_batch) throw Error(GCK_E_INVALID_ARGUMENT, "submitted batch above max_batch");
+  hipStream_t st = host ? w->stream : (hipStream_t)stream;
+  stage_caveats(*w, cav_table, n_ctx, st);
+  if (now_us == 0) now_us = wall_now_us();
+  submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host);
+}
+
+// Completes a submitted batch. Takes no engine lock: a writer that wants to replace the
+// snapshot finishes the batch first (drain_batches, under w->m), so the snapshot cannot change
+// while this runs the later stages.
+void device_wait(Engine& e, Workspace* w) {
+  HIP_OK(hipSetDevice(e.device));
+  std::lock_guard<std::mutex> lk(w->m);
+  finish_batch(e, *w);  // no-op when a writer already finished it (drain_batches)
+  w->state = 0;
+  if (w->fail_code) throw Error(w->fail_code, w->fail_msg);
+  copy_out(*w);
+  std::lock_guard<std::mutex> sl(e.stats_mu);
+  e.stats.kernel_ms = w->b_ms;
+}
+
+// Synchronous batches over device buffers on one held workspace (lookups).
+static void check_range(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
+                        int32_t* d_err, hipStream_t st, float* ms) {
+  for (size_t pos = 0; pos < n; pos += w.max_batch) {
+    const uint32_t len = (uint32_t)std::min(n - pos, w.max_batch);
+    submit_batch(e, w, d_items + pos, len, now_us, d_perm + pos, d_err + pos, st, false);
+    finish_batch(e, w);
+    w.state = 0;
+    *ms += w.b_ms;
+  }
+}
+
+// The partitioned batch's workspace: its own, outside the pool (a partitioned batch spans many
+// calls, one BFS level each).
+static Workspace& part_workspace(Engine& e) {
+  std::lock_guard<std::mutex> lk(e.ws_mu);
+  if (!e.part_ws) e.part_ws = create_workspace(e);
+  ensure_wide(*e.part_ws);
+  return *e.part_ws;
 }
 
 #include "partition.inc"

@@ -3,6 +3,7 @@
 #pragma once
 #include <cstdint>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
@@ -158,11 +159,18 @@ struct Engine {
   uint64_t seq = 0;
   // committed
   uint64_t revision = 0;
+  uint64_t head_revision = 0;  // consistency.Full target (gck_set_head_revision; 0 = local head)
   uint64_t n_tuples = 0;
   bool committed = false;
   DeviceSnapshot* dev = nullptr;
+  // check workspaces (engine.hip acquire_ws): one per batch in flight, at most
+  // cfg.workspaces (0 = 4); ws_cv signals a released one
   std::mutex ws_mu;
-  Workspace* ws = nullptr;
+  std::condition_variable ws_cv;
+  std::vector<Workspace*> ws_pool;
+  Workspace* part_ws = nullptr;   // the partitioned batch's own workspace (partition.inc)
+  uint64_t part_generation = 0;   // the snapshot generation a partitioned batch started on
+  std::mutex stats_mu;            // stats are added by concurrent batches
   uint64_t generation = 0;        // bumped by every device snapshot (commit, Watch batch)
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
@@ -192,17 +200,41 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta = false);
 void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
 // cav_table: the call's caveat outcome table (row = partial instance, n_ctx columns = check
 // contexts 1..n_ctx; empty when the call has no check contexts)
-void device_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us,
+// Pooled check workspaces (one per batch in flight, at most cfg.workspaces): acquire waits for
+// a free one. Callers take their workspaces BEFORE the engine lock (the holders of busy ones
+// may need the lock to finish their batches).
+Workspace* acquire_ws(Engine& e);
+void release_ws(Engine& e, Workspace* w);
+struct WsLease {
+  Engine& e;
+  Workspace* w;
+  explicit WsLease(Engine& en) : e(en), w(acquire_ws(en)) {}
+  ~WsLease() { release_ws(e, w); }
+  WsLease(const WsLease&) = delete;
+  WsLease& operator=(const WsLease&) = delete;
+};
+void device_check(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us,
                   uint8_t* d_perm, int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table,
                   uint32_t n_ctx);
-void device_check_host(Engine& e, const gck_item* items, size_t n, int64_t now_us,
+// Host buffers, chunks of max_batch alternating over w0 and w1 (w1 may be null or w0).
+void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* items, size_t n, int64_t now_us,
                        uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
+// Asynchronous batches (gck_check_submit / gck_check_wait): submit starts one batch (n <=
+// max_batch) on an acquired workspace; wait finishes it (later stages, results copied out) —
+// the caller then releases the workspace. `items` etc. are device pointers on `stream`
+// (host == false) or host buffers (host == true: the workspace's own stream).
+void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
+                   int32_t* err, void* stream, bool host, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
+void device_wait(Engine& e, Workspace* w);
+// Finishes every batch in flight (a writer holding the engine exclusively calls this before
+// it replaces the snapshot: the batches keep the results of the snapshot they started on).
+void drain_batches(Engine& e);
 uint64_t device_bytes(const Engine& e);
 void device_export(Engine& e, std::vector<HostCSR>& out);
 // lookups (lookup.inc): candidates [0, n) of the varying id of `proto` (resource id when
 // vary_res, else subject id); matching ids ascending with their permissionship
-void device_lookup(Engine& e, const gck_item& proto, bool vary_res, uint32_t n_candidates, int64_t now_us,
-                   std::vector<uint32_t>& ids, std::vector<uint8_t>& perms);
+void device_lookup(Engine& e, Workspace& w, const gck_item& proto, bool vary_res, uint32_t n_candidates,
+                   int64_t now_us, std::vector<uint32_t>& ids, std::vector<uint8_t>& perms);
 // partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
 void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
 void part_expand(Engine& e, uint64_t* send_counts);

@@ -157,6 +157,7 @@ int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null schema text");
     auto sc = compile_schema(std::string(text ? text : "", len));
     std::unique_lock<std::shared_mutex> lk(e.mu);
+    drain_batches(e);
     e.schema = std::move(sc);
     e.schema_text.assign(text ? text : "", len);
     e.interner.assign(e.schema->types.size(), TypeInterner());
@@ -379,6 +380,7 @@ int gck_commit_snapshot(gck_engine* ge) {
     need_schema(e);
     REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
     std::unique_lock<std::shared_mutex> lk(e.mu);
+    drain_batches(e);
     std::vector<HostCSR> csrs = build_csrs(e);
     device_upload(e, csrs);  // device-pointer CSRs are copied before the caller regains control
     e.staged.clear();
@@ -404,6 +406,7 @@ int gck_load_snapshot_file(gck_engine* ge, const char* path) {
     need_schema(e);
     REQUIRE(path, GCK_E_INVALID_ARGUMENT, "null path");
     std::unique_lock<std::shared_mutex> lk(e.mu);
+    drain_batches(e);
     load_snapshot_file(e, path);
   });
 }
@@ -412,7 +415,16 @@ int gck_revision(gck_engine* ge, uint64_t* out) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    std::shared_lock<std::shared_mutex> lk(e.mu);
     *out = e.revision;
+  });
+}
+
+int gck_set_head_revision(gck_engine* ge, uint64_t revision) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    if (revision > e.head_revision) e.head_revision = revision;  // the head only moves forward
   });
 }
 
@@ -464,6 +476,7 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
     need_schema(e);
     REQUIRE(n == 0 || updates, GCK_E_INVALID_ARGUMENT, "null updates");
     std::unique_lock<std::shared_mutex> lk(e.mu);
+    drain_batches(e);
     apply_updates(e, revision, std::vector<gck_update>(updates, updates + n));
   });
 }
@@ -475,17 +488,26 @@ int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, 
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
     std::unique_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    drain_batches(e);
     std::vector<gck_update> ups;
     parse_updates_text(e, text, len, ups);
     apply_updates(e, revision, ups);
   });
 }
 
+// consistency.Strategy (consistency/consistency.go:15-77) against the applied revision. A
+// requirement the snapshot has not reached yet is GCK_E_REVISION (gRPC Unavailable: the client
+// retries, client/client.go:193-211, while the Watch stream catches up); a Snapshot revision the
+// snapshot has moved past can never be served here (no MVCC on the device) and is permanent.
 static void check_consistency(Engine& e, const gck_consistency* cs) {
   if (!cs) return;
   switch (cs->requirement) {
     case GCK_CONSISTENCY_MIN_LATENCY:
-    case GCK_CONSISTENCY_FULL:  // the local snapshot is the head of this evaluator
+      return;
+    case GCK_CONSISTENCY_FULL:
+      REQUIRE(e.revision >= e.head_revision, GCK_E_REVISION,
+              "snapshot revision " + std::to_string(e.revision) + " has not reached the head revision " +
+                  std::to_string(e.head_revision));
       return;
     case GCK_CONSISTENCY_AT_LEAST:
       REQUIRE(e.revision >= cs->revision, GCK_E_REVISION,
@@ -493,8 +515,11 @@ static void check_consistency(Engine& e, const gck_consistency* cs) {
                   std::to_string(cs->revision));
       return;
     case GCK_CONSISTENCY_SNAPSHOT:
+      REQUIRE(e.revision <= cs->revision, GCK_E_REVISION_GONE,
+              "snapshot revision " + std::to_string(cs->revision) + " is no longer available (the local snapshot is at " +
+                  std::to_string(e.revision) + ")");
       REQUIRE(e.revision == cs->revision, GCK_E_REVISION,
-              "snapshot revision " + std::to_string(e.revision) + " != requested " +
+              "snapshot revision " + std::to_string(e.revision) + " has not reached the requested " +
                   std::to_string(cs->revision));
       return;
     default:
@@ -502,25 +527,50 @@ static void check_consistency(Engine& e, const gck_consistency* cs) {
   }
 }
 
+// State errors before any workspace is taken (a workspace needs the device the first commit set
+// up): no snapshot, or a partitioned engine.
+static void precheck(Engine& e) {
+  std::shared_lock<std::shared_mutex> lk(e.mu);
+  REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+  REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
+}
+
+// The checks common to every check entry point (under the shared engine lock).
+static void check_request(Engine& e, const gck_consistency* cs, const gck_item* items, size_t n, bool host_items,
+                          const char* const* contexts, const size_t* context_lens, size_t n_contexts) {
+  REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+  REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
+  REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
+  REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
+  check_consistency(e, cs);
+  if (host_items)
+    for (size_t i = 0; i < n; ++i)
+      REQUIRE(items[i].context_slot <= n_contexts, GCK_E_INVALID_ARGUMENT,
+              "item " + std::to_string(i) + ": context_slot " + std::to_string(items[i].context_slot) +
+                  " beyond the " + std::to_string(n_contexts) + " contexts given");
+}
+
 int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
                        const char* const* contexts, const size_t* context_lens, size_t n_contexts,
                        int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
   return guard([&] {
     Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
-    REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
-    REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
-    REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
-    check_consistency(e, cs);
-    if (n == 0) return;  // empty request -> empty response (client/client_test.go:203-207)
-    for (size_t i = 0; i < n; ++i)
-      REQUIRE(items[i].context_slot <= n_contexts, GCK_E_INVALID_ARGUMENT,
-              "item " + std::to_string(i) + ": context_slot " + std::to_string(items[i].context_slot) +
-                  " beyond the " + std::to_string(n_contexts) + " contexts given");
+    if (n == 0) {  // empty request -> empty response (client/client_test.go:203-207)
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      check_request(e, cs, items, 0, true, contexts, context_lens, n_contexts);
+      return;
+    }
+    // workspaces first, then the engine lock (engine.hpp WsLease)
+    precheck(e);
+    const size_t mb = e.cfg.max_batch ? e.cfg.max_batch : 65536;
+    WsLease l0(e);
+    std::unique_ptr<WsLease> l1;
+    if (n > mb) l1.reset(new WsLease(e));
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    check_request(e, cs, items, n, true, contexts, context_lens, n_contexts);
     const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
-    device_check_host(e, items, n, now_us, out_perm, out_err, table, (uint32_t)n_contexts);
+    device_check_host(e, l0.w, l1 ? l1->w : nullptr, items, n, now_us, out_perm, out_err, table, (uint32_t)n_contexts);
   });
 }
 
@@ -534,15 +584,18 @@ int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n,
                               uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
   return guard([&] {
     Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
-    REQUIRE(n_contexts == 0 || (contexts && context_lens), GCK_E_INVALID_ARGUMENT, "null contexts");
-    REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
-    REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
-    if (n == 0) return;
+    if (n == 0) {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      check_request(e, nullptr, nullptr, 0, false, contexts, context_lens, n_contexts);
+      return;
+    }
+    precheck(e);
+    WsLease l0(e);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    check_request(e, nullptr, nullptr, 0, false, contexts, context_lens, n_contexts);
     const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
-    device_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream, table, (uint32_t)n_contexts);
+    device_check(e, *l0.w, d_items, n, now_us, d_out_perm, d_out_err, stream, table, (uint32_t)n_contexts);
   });
 }
 
@@ -551,12 +604,74 @@ int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int
   return gck_check_bulk_device_ctx(ge, d_items, n, nullptr, nullptr, 0, now_us, d_out_perm, d_out_err, stream);
 }
 
+// A submitted batch: the workspace it holds (returned to the pool by the wait), or, for an empty
+// batch, nothing to do.
+struct gck_batch {
+  Workspace* w = nullptr;
+};
+
+int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                     const char* const* contexts, const size_t* context_lens, size_t n_contexts, int64_t now_us,
+                     uint8_t* out_perm, int32_t* out_err, uint32_t flags, void* stream, gck_batch** out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    const bool host = !(flags & GCK_SUBMIT_DEVICE);
+    auto* b = new gck_batch();
+    if (n == 0) {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      try {
+        check_request(e, cs, items, 0, host, contexts, context_lens, n_contexts);
+      } catch (...) {
+        delete b;
+        throw;
+      }
+      *out = b;
+      return;
+    }
+    precheck(e);
+    Workspace* w = acquire_ws(e);  // before the engine lock (engine.hpp WsLease)
+    try {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      check_request(e, cs, items, n, host, contexts, context_lens, n_contexts);
+      const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
+      device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host, table, (uint32_t)n_contexts);
+    } catch (...) {
+      release_ws(e, w);
+      delete b;
+      throw;
+    }
+    b->w = w;
+    *out = b;
+  });
+}
+
+int gck_check_wait(gck_engine* ge, gck_batch* b) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(b, GCK_E_INVALID_ARGUMENT, "null batch");
+    std::unique_ptr<gck_batch> own(b);
+    if (!b->w) return;
+    Workspace* w = b->w;
+    try {
+      device_wait(e, w);
+    } catch (...) {
+      release_ws(e, w);
+      throw;
+    }
+    release_ws(e, w);
+  });
+}
+
 int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(world >= 1 && world <= 63 && rank < world, GCK_E_INVALID_ARGUMENT, "bad rank / world");
     std::unique_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(!e.committed && !e.dev && !e.ws, GCK_E_STATE, "gck_set_partition must precede the first snapshot");
+    REQUIRE(!e.committed && !e.dev && e.ws_pool.empty() && !e.part_ws, GCK_E_STATE,
+            "gck_set_partition must precede the first snapshot");
     e.part_rank = rank;
     e.part_world = world;
     if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR;  // both need the whole graph
@@ -621,11 +736,12 @@ int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
   });
 }
 
-// The result of the last lookup of this thread, so a caller whose buffer was too small gets it
-// on the retry without a second sweep.
+// The result of a lookup that did not fit the caller's buffer, kept per thread so that the retry
+// with cap >= *out_n copies it out without a second sweep. It matches only a retry of the same
+// request on the same snapshot (process-wide snapshot generation) at the same explicit now_us
+// (now_us = 0, the wall clock, never matches), and is dropped once copied out.
 struct LookupCache {
-  const gck_engine* e = nullptr;
-  uint64_t generation = 0;
+  uint64_t generation = 0;  // 0 = empty
   gck_item proto{};
   bool vary_res = false;
   int64_t now_us = 0;
@@ -637,9 +753,15 @@ thread_local LookupCache g_lookup;
 static void lookup(gck_engine* ge, const gck_consistency* cs, const gck_item& proto, bool vary_res, int64_t now_us,
                    uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n) {
   Engine& e = need(ge);
+  REQUIRE(out_n && (cap == 0 || (out_ids && out_perm)), GCK_E_INVALID_ARGUMENT, "null buffers");
+  {
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(e.part_world <= 1, GCK_E_STATE, "lookups are not available on a partitioned engine");
+  }
+  WsLease lease(e);  // before the engine lock (engine.hpp WsLease)
   std::shared_lock<std::shared_mutex> lk(e.mu);
   REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
-  REQUIRE(out_n && (cap == 0 || (out_ids && out_perm)), GCK_E_INVALID_ARGUMENT, "null buffers");
   REQUIRE(e.part_world <= 1, GCK_E_STATE, "lookups are not available on a partitioned engine");
   check_consistency(e, cs);
   const Schema& sc = *e.schema;
@@ -650,13 +772,13 @@ static void lookup(gck_engine* ge, const gck_consistency* cs, const gck_item& pr
   REQUIRE(proto.subject_relation == GCK_ELLIPSIS ||
               (proto.subject_relation < sc.rels.size() && sc.rels[proto.subject_relation].type == proto.subject_type),
           GCK_E_NOT_FOUND, "subject relation not found");
-  const bool hit = g_lookup.e == ge && g_lookup.generation == e.generation && g_lookup.vary_res == vary_res &&
-                   g_lookup.now_us == now_us && std::memcmp(&g_lookup.proto, &proto, sizeof(gck_item)) == 0;
+  const bool hit = now_us != 0 && g_lookup.generation != 0 && g_lookup.generation == e.generation &&
+                   g_lookup.vary_res == vary_res && g_lookup.now_us == now_us &&
+                   std::memcmp(&g_lookup.proto, &proto, sizeof(gck_item)) == 0;
   if (!hit) {
-    g_lookup.e = nullptr;
+    g_lookup.generation = 0;
     const uint32_t n = e.interner[vary_res ? proto.resource_type : proto.subject_type].count;
-    device_lookup(e, proto, vary_res, n, now_us, g_lookup.ids, g_lookup.perms);
-    g_lookup.e = ge;
+    device_lookup(e, *lease.w, proto, vary_res, n, now_us, g_lookup.ids, g_lookup.perms);
     g_lookup.generation = e.generation;
     g_lookup.proto = proto;
     g_lookup.vary_res = vary_res;
@@ -669,6 +791,9 @@ static void lookup(gck_engine* ge, const gck_consistency* cs, const gck_item& pr
     std::memcpy(out_ids, g_lookup.ids.data(), g_lookup.ids.size() * 4);
     std::memcpy(out_perm, g_lookup.perms.data(), g_lookup.perms.size());
   }
+  g_lookup.generation = 0;
+  g_lookup.ids.clear();
+  g_lookup.perms.clear();
 }
 
 int gck_lookup_resources(gck_engine* ge, const gck_consistency* cs, uint16_t resource_type, uint16_t permission,

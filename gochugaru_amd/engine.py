@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import time
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -26,6 +27,7 @@ GCK_E_CAPACITY = -5
 GCK_E_STATE = -6
 GCK_E_REVISION = -7
 GCK_E_NO_DEVICE = -8
+GCK_E_REVISION_GONE = -9
 
 PERM_UNSPECIFIED, PERM_NO, PERM_HAS, PERM_CONDITIONAL = 0, 1, 2, 3
 
@@ -51,6 +53,7 @@ FLAG_NO_BUNDLE = 2
 FLAG_NO_MHASH = 4
 FLAG_NO_GIANT = 8
 FLAG_NO_BIDIR = 16
+SUBMIT_DEVICE = 1
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -96,7 +99,7 @@ class _Config(C.Structure):
                 ("bundle_waves_per_cu", C.c_uint32), ("bundle_budget", C.c_uint32),
                 ("giant_frontier", C.c_uint32), ("giant_visited", C.c_uint32),
                 ("giant_slots", C.c_uint32), ("bidir_both", C.c_uint32),
-                ("reserved0", C.c_uint32)]
+                ("workspaces", C.c_uint32)]
 
 
 class _Consistency(C.Structure):
@@ -147,6 +150,7 @@ _SIGS = {
     "gck_save_snapshot": (C.c_int, [_P, C.c_char_p]),
     "gck_load_snapshot_file": (C.c_int, [_P, C.c_char_p]),
     "gck_revision": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "gck_set_head_revision": (C.c_int, [_P, C.c_uint64]),
     "gck_tuple_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_device_bytes": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_apply_updates": (C.c_int, [_P, C.c_uint64, _P, C.c_size_t]),
@@ -157,6 +161,10 @@ _SIGS = {
                                      C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P]),
     "gck_check_bulk_device_ctx": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
                                             C.c_size_t, C.c_int64, _P, _P, _P]),
+    "gck_check_submit": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.POINTER(C.c_char_p),
+                                   C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P, C.c_uint32, _P,
+                                   C.POINTER(_P)]),
+    "gck_check_wait": (C.c_int, [_P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
     "gck_lookup_resources": (C.c_int, [_P, C.POINTER(_Consistency), C.c_uint16, C.c_uint16, C.c_uint16,
                                        C.c_uint16, C.c_uint32, C.c_int64, _P, _P, C.c_size_t,
@@ -224,7 +232,7 @@ class Engine:
                  bundle_visited: int = 0, bundle_waves_per_cu: int = 0,
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
                  giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
-                 bidir: bool = True, bidir_both: int = 0):
+                 bidir: bool = True, bidir_both: int = 0, workspaces: int = 0):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
                  | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
@@ -232,7 +240,7 @@ class Engine:
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,
-                      giant_visited, giant_slots, bidir_both, 0)
+                      giant_visited, giant_slots, bidir_both, workspaces)
         h = _P()
         _check(lib.gck_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -384,6 +392,11 @@ class Engine:
         _check(self._lib.gck_revision(self._h, C.byref(out)))
         return out.value
 
+    def set_head_revision(self, revision: int):
+        """The source's head revision for consistency.Full() (ReadSchema's ReadAt token,
+        client/client.go:416-422, or a Watch checkpoint)."""
+        _check(self._lib.gck_set_head_revision(self._h, revision))
+
     @property
     def tuple_count(self) -> int:
         out = C.c_uint64()
@@ -433,6 +446,29 @@ class Engine:
         _check(self._lib.gck_check_bulk_device_ctx(self._h, d_items, n, ctx_arr, ctx_lens, n_ctx, now_us,
                                                    d_perm, d_err, stream))
 
+    def submit(self, items, n: Optional[int] = None, out_perm=None, out_err=None, requirement: int = CONSISTENCY_MIN_LATENCY,
+               revision: int = 0, now_us: int = 0, contexts: Optional[Sequence] = None, device: bool = False,
+               stream: Optional[int] = None) -> "Batch":
+        """Starts one batch (n <= max_batch) without waiting (gck_check_submit); Batch.wait()
+        completes it. Host batches: `items` is an ITEM_DTYPE array and the results are returned by
+        wait(). Device batches (device=True): `items`, `out_perm`, `out_err` are device pointers
+        ordered on `stream`."""
+        cs = _Consistency(requirement, 0, revision)
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        h = _P()
+        if device:
+            _check(self._lib.gck_check_submit(self._h, C.byref(cs), items, n, ctx_arr, ctx_lens, n_ctx, now_us,
+                                              out_perm, out_err, SUBMIT_DEVICE, stream, C.byref(h)))
+            return Batch(self, h, None, None, None)
+        items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
+        n = len(items)
+        perm = np.zeros(n, dtype=np.uint8)
+        err = np.zeros(n, dtype=np.int32)
+        _check(self._lib.gck_check_submit(self._h, C.byref(cs), items.ctypes.data if n else None, n, ctx_arr,
+                                          ctx_lens, n_ctx, now_us, perm.ctypes.data if n else None,
+                                          err.ctypes.data if n else None, 0, None, C.byref(h)))
+        return Batch(self, h, perm, err, items)
+
     # ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) --------
     def _lookup(self, fn, args, requirement, revision):
         cs = _Consistency(requirement, 0, revision)
@@ -453,6 +489,8 @@ class Engine:
                          now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
         """Ids (ascending) of the resource_type objects the subject has `permission` on, and
         their permissionship (PERM_HAS / PERM_CONDITIONAL)."""
+        # an explicit evaluation time, so that a capacity retry is served from the engine's cache
+        now_us = now_us or time.time_ns() // 1000
         return self._lookup(self._lib.gck_lookup_resources,
                             (resource_type, permission, subject_type, subject_relation, subject_id, now_us),
                             requirement, revision)
@@ -461,6 +499,7 @@ class Engine:
                         subject_relation: int = ELLIPSIS, requirement: int = CONSISTENCY_MIN_LATENCY,
                         revision: int = 0, now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
         """Ids (ascending) of the subject_type subjects that have `permission` on the resource."""
+        now_us = now_us or time.time_ns() // 1000
         return self._lookup(self._lib.gck_lookup_subjects,
                             (resource_type, resource_id, permission, subject_type, subject_relation, now_us),
                             requirement, revision)
@@ -550,6 +589,27 @@ class Engine:
             if items[i]["subject_type"] == TYPE_INVALID:
                 items[i]["subject_id"] = ID_WILDCARD if r.SubjectID == "*" else ID_ABSENT
         return items
+
+
+class Batch:
+    """A submitted batch (gck_batch): wait() completes it exactly once."""
+
+    def __init__(self, engine, handle, perm, err, items):
+        self._engine, self._h = engine, handle
+        self.perm, self.err = perm, err
+        self._items = items  # host items stay alive until the wait (they are staged at submit anyway)
+
+    def wait(self):
+        if self._h is not None:
+            h, self._h = self._h, None
+            _check(self._engine._lib.gck_check_wait(self._engine._h, h))
+        return self.perm, self.err
+
+    def __del__(self):
+        try:
+            self.wait()
+        except Exception:
+            pass
 
 
 def _context_json(ctx) -> str:

@@ -29,10 +29,23 @@
  *       honour consistency.Strategy (consistency/consistency.go:15-77) as sent in
  *       CheckBulkPermissionsRequest.Consistency (client/client.go:263).
  *
+ *   gck_check_submit / gck_check_wait
+ *       the same round-trip split in two, so that a caller keeps several CheckBulkPermissions
+ *       batches in flight (Client.CheckIter's chunks, client/client.go:164-180, or concurrent
+ *       Client.Check calls) and the device overlaps them.
+ *   gck_set_head_revision
+ *       the revision consistency.Full() (consistency/consistency.go:25-35) must reach: the
+ *       ReadAt token of Client.ReadSchema (client/client.go:416-422) or a Watch checkpoint.
+ *
  * Ownership: all inputs and outputs are caller-allocated; the engine never retains a caller
- * pointer after a call returns. Return value: GCK_OK (0) or a negative GCK_E_* status; the
- * message is available from gck_last_error() (thread-local).
- * Threading: gck_check_bulk* may be called concurrently; snapshot/schema calls are exclusive.
+ * pointer after a call returns, except that gck_check_submit keeps the output pointers (and, for
+ * device batches, the item pointer) until the matching gck_check_wait. Return value: GCK_OK (0)
+ * or a negative GCK_E_* status; the message is available from gck_last_error() (thread-local).
+ * Threading: gck_check_bulk*, gck_check_submit / gck_check_wait and the lookups may be called
+ * concurrently from any number of threads: each batch in flight runs on its own pooled
+ * workspace and HIP stream (gck_config.workspaces of them; a call waits for a free one).
+ * Schema, snapshot and Watch calls are exclusive: they first finish every batch in flight,
+ * which keeps the results of the snapshot it was submitted against.
  */
 #ifndef GCK_H
 #define GCK_H
@@ -44,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 4
+#define GCK_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -56,6 +69,8 @@ extern "C" {
 #define GCK_E_STATE (-6)            /* wrong call order (no schema / no snapshot) */
 #define GCK_E_REVISION (-7)         /* consistency requirement not satisfiable locally */
 #define GCK_E_NO_DEVICE (-8)        /* no HIP device / HIP runtime unavailable */
+#define GCK_E_REVISION_GONE (-9)    /* consistency.Snapshot at a revision the snapshot has moved past:
+                                       permanent (SpiceDB: FailedPrecondition), not retriable */
 
 /* ---- Permissionship (authzed v1 CheckPermissionResponse.Permissionship) --------------- */
 #define GCK_PERM_UNSPECIFIED 0
@@ -114,7 +129,8 @@ typedef struct gck_config {
   uint32_t giant_slots;        /* resident workgroup bundles; 0 = one per CU */
   uint32_t bidir_both;         /* bidirectional checks expand both sides while their two
                                   frontiers hold at most this many entries; 0 = 64 */
-  uint32_t reserved0;
+  uint32_t workspaces;         /* check batches in flight at once (concurrent callers and
+                                  submitted batches), one device workspace each; 0 = 4 */
 } gck_config;
 
 /* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
@@ -237,6 +253,11 @@ int gck_commit_snapshot(gck_engine* e);
 int gck_save_snapshot(gck_engine* e, const char* path);
 int gck_load_snapshot_file(gck_engine* e, const char* path);
 int gck_revision(gck_engine* e, uint64_t* out);
+/* The source's head revision, for consistency.Full(): a Full check (or lookup) returns
+ * GCK_E_REVISION — gRPC Unavailable, which the client retries — until the applied revision
+ * (gck_commit_snapshot / gck_apply_updates) reaches it. 0 (the default) = the local snapshot is
+ * the head. The head only moves forward. */
+int gck_set_head_revision(gck_engine* e, uint64_t revision);
 int gck_tuple_count(gck_engine* e, uint64_t* out);
 /* Bytes resident in HBM for the snapshot (CSR + tables). */
 int gck_device_bytes(gck_engine* e, uint64_t* out);
@@ -280,6 +301,20 @@ int gck_check_bulk_device(gck_engine* e, const gck_item* d_items, size_t n, int6
 int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
                               const char* const* contexts, const size_t* context_lens, size_t n_contexts,
                               int64_t now_us, uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
+/* Asynchronous batches: gck_check_submit starts one batch of n <= max_batch items and returns at
+ * once with a handle; gck_check_wait(handle) completes it (results written, handle consumed).
+ * Every submitted batch must be waited for exactly once. GCK_SUBMIT_DEVICE: items / out_perm /
+ * out_err are device buffers ordered on `stream` (as gck_check_bulk_device_ctx); otherwise they
+ * are host buffers (the items are staged before the call returns; the outputs are written by the
+ * wait). Consistency is checked at submit; the batch sees the snapshot current at submit, even if
+ * a Watch batch is applied before the wait. */
+typedef struct gck_batch gck_batch;
+#define GCK_SUBMIT_DEVICE 1u
+int gck_check_submit(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
+                     const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                     int64_t now_us, uint8_t* out_perm, int32_t* out_err, uint32_t flags, void* stream,
+                     gck_batch** out);
+int gck_check_wait(gck_engine* e, gck_batch* batch);
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
 

@@ -1,0 +1,227 @@
+"""Concurrent and asynchronous checks on one engine (include/gck.h threading contract): pooled
+workspaces, gck_check_submit / gck_check_wait, checks racing Watch batches, consistency waits
+(consistency.Full after gck_set_head_revision, AtLeast) that the client's retry
+(client/client.go:193-211) carries over, and the permanent error for a Snapshot revision the
+engine has moved past. Every result is compared with the oracle."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from gochugaru_amd import consistency, rel
+from gochugaru_amd import engine as E
+from gochugaru_amd.client import Client
+from tests import gen
+from tests.helpers import oracle_for, parse_check, to_oracle_item
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(schema, tuples, revision=1, **kw):
+    e = E.Engine(**kw)
+    e.load_schema(schema)
+    e.load_snapshot_text(revision, "\n".join(tuples))
+    return e
+
+
+def _want(schema, tuples, checks):
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    return [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+
+
+def _got(perm, err):
+    return [(int(p), int(x)) for p, x in zip(perm, err)]
+
+
+@pytest.mark.parametrize("workspaces", [1, 2, 4])
+def test_concurrent_callers(workspaces):
+    """Four threads, each its own batches of a different family's checks (one engine, one graph
+    per family): every result equals the oracle whatever the interleaving."""
+    schema, tuples, checks = gen.gdocs(5)
+    e = _engine(schema, tuples, workspaces=workspaces)
+    want = _want(schema, tuples, checks)
+    items = e.make_items([parse_check(c) for c in checks])
+    rng = np.random.default_rng(7)
+    orders = [rng.permutation(len(checks)) for _ in range(4)]
+    errors, results = [], [None] * 4
+
+    def worker(k):
+        try:
+            out = []
+            for rep in range(6):
+                idx = orders[k] if rep % 2 else orders[k][::-1]
+                perm, err = e.check_bulk(items[idx], now_us=gen.NOW_US)
+                got = _got(perm, err)
+                out.append(all(got[i] == want[j] for i, j in enumerate(idx)))
+            results[k] = out
+        except Exception as ex:  # noqa: BLE001
+            errors.append(ex)
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert all(r is not None and all(r) for r in results), results
+    e.close()
+
+
+def test_submit_wait_host_and_device():
+    import torch
+    schema, tuples, checks = gen.github(3)
+    e = _engine(schema, tuples, workspaces=3)
+    want = _want(schema, tuples, checks)
+    items = e.make_items([parse_check(c) for c in checks])
+    # three host batches in flight, waited for out of order
+    bs = [e.submit(items[k::3], now_us=gen.NOW_US) for k in range(3)]
+    for k in (2, 0, 1):
+        perm, err = bs[k].wait()
+        assert _got(perm, err) == want[k::3]
+    # device batches on two streams
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    n = len(items)
+    outs = []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        perm = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        err = torch.zeros(n, dtype=torch.int32, device="cuda")
+        b = e.submit(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us=gen.NOW_US, device=True,
+                     stream=s.cuda_stream)
+        outs.append((b, perm, err, s))
+    for b, perm, err, s in outs:
+        b.wait()
+        s.synchronize()
+        assert _got(perm.cpu().numpy(), err.cpu().numpy()) == want
+    # more batches than workspaces: submit blocks until one is released by a wait... so wait in
+    # turn (a 4th submit before any wait would block this thread forever by design)
+    for _ in range(3):
+        b = e.submit(items, now_us=gen.NOW_US)
+        assert _got(*b.wait()) == want
+    e.close()
+
+
+def test_submitted_batch_keeps_its_snapshot_across_a_watch_batch():
+    """A batch submitted at revision 1 and waited for after a Watch batch moved the snapshot
+    to revision 2 answers for revision 1 (the writer finishes it before the swap)."""
+    schema, tuples, checks = gen.nested(4)
+    e = _engine(schema, tuples, workspaces=2)
+    items = e.make_items([parse_check(c) for c in checks])
+    want1 = _want(schema, tuples, checks)
+    # delete every direct user membership of one group layer: many answers change
+    gone = [t for t in tuples if t.startswith("group:g1") and "@user:" in t]
+    later = [t for t in tuples if t not in gone]
+    want2 = _want(schema, later, checks)
+    assert want1 != want2
+    b = e.submit(items, now_us=gen.NOW_US)
+    e.apply_updates_text(2, "\n".join("DELETE " + t for t in gone))
+    assert _got(*b.wait()) == want1
+    perm, err = e.check_bulk(items, now_us=gen.NOW_US)
+    assert _got(perm, err) == want2
+    e.close()
+
+
+def test_checks_racing_watch_batches():
+    """One thread applies Watch batches (add / remove a chain link) while another checks: every
+    check batch equals the oracle of one of the two states (a batch never sees half a Watch
+    batch)."""
+    schema, tuples, checks = gen.nested(9)
+    e = _engine(schema, tuples, workspaces=2)
+    items = e.make_items([parse_check(c) for c in checks])
+    link = [t for t in tuples if "#member@group:" in t][:20]
+    base = [t for t in tuples if t not in link]
+    want_a, want_b = _want(schema, tuples, checks), _want(schema, base, checks)
+    stop = threading.Event()
+    errors = []
+
+    def writer():
+        try:
+            rev = 1
+            while not stop.is_set():
+                rev += 1
+                e.apply_updates_text(rev, "\n".join("DELETE " + t for t in link))
+                rev += 1
+                e.apply_updates_text(rev, "\n".join("CREATE " + t for t in link))
+        except Exception as ex:  # noqa: BLE001
+            errors.append(ex)
+
+    t = threading.Thread(target=writer)
+    t.start()
+    seen = set()
+    try:
+        for _ in range(40):
+            got = _got(*e.check_bulk(items, now_us=gen.NOW_US))
+            assert got in (want_a, want_b)
+            seen.add(got == want_a)
+    finally:
+        stop.set()
+        t.join(timeout=60)
+    assert not errors, errors
+    e.close()
+
+
+def test_full_consistency_waits_for_the_head_revision():
+    """consistency.Full after SetHeadRevision(3): Unavailable (retried by the client's backoff)
+    until a Watch batch moves the snapshot to revision 3, then the answer of revision 3."""
+    schema = "definition user {}\ndefinition document { relation reader: user\n permission view = reader }"
+    e = _engine(schema, ["document:d#reader@user:a"], revision=1)
+    c = Client(e)
+    c.SetHeadRevision(3)
+    r = rel.MustFromTriple("document:d", "view", "user:b")
+    ctx = consistency.Context(metadata={})
+    object.__setattr__(ctx, "deadline", 0)
+    ok, err = c.CheckOne(ctx, consistency.Full(), r)  # no retry: the error itself
+    assert ok is False and isinstance(err, E.GckError) and err.code == E.GCK_E_REVISION
+    assert c.CheckOne(None, consistency.MinLatency(), r) == (False, None)
+
+    def watch():
+        time.sleep(0.3)
+        e.apply_updates_text(2, "")
+        time.sleep(0.2)
+        e.apply_updates_text(3, "CREATE document:d#reader@user:b")
+
+    t = threading.Thread(target=watch)
+    t0 = time.monotonic()
+    t.start()
+    assert c.CheckOne(None, consistency.Full(), r) == (True, None)  # retried until revision 3
+    assert time.monotonic() - t0 >= 0.45
+    t.join()
+    # AtLeast behaves the same way
+    t = threading.Thread(target=lambda: (time.sleep(0.2), e.apply_updates_text(4, "DELETE document:d#reader@user:b")))
+    t.start()
+    assert c.CheckOne(None, consistency.AtLeast("4"), r) == (False, None)
+    t.join()
+    e.close()
+
+
+def test_snapshot_revision_passed_is_permanent():
+    schema = "definition user {}\ndefinition document { relation reader: user }"
+    e = _engine(schema, ["document:d#reader@user:a"], revision=5)
+    c = Client(e)
+    r = rel.MustFromTriple("document:d", "reader", "user:a")
+    t0 = time.monotonic()
+    ok, err = c.CheckOne(None, consistency.Snapshot("4"), r)  # no retry, no 15-minute backoff
+    assert time.monotonic() - t0 < 1.0
+    assert ok is False and isinstance(err, E.GckError) and err.code == E.GCK_E_REVISION_GONE
+    assert c.CheckOne(None, consistency.Snapshot("5"), r) == (True, None)
+    e.close()
+
+
+def test_lookup_sees_expiration_between_calls():
+    """two lookups on one snapshot at wall-clock time; a relationship that expires
+    between them must disappear from the second."""
+    schema = ("definition user {}\ndefinition document {\n relation reader: user with expiration\n"
+              " permission view = reader\n}\nuse expiration")
+    soon = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() + 2))
+    e = _engine(schema, [f"document:a#reader@user:u[expiration:{soon}]", "document:b#reader@user:u"])
+    rt, st = e.type_id("document"), e.type_id("user")
+    view = e.relation_id(rt, "view")
+    uid = int(e.intern(st, ["u"])[0])
+    ids1, _ = e.lookup_resources(rt, view, st, E.ELLIPSIS, uid)
+    time.sleep(3.2)  # past the expiration (whole seconds in the text form)
+    ids2, _ = e.lookup_resources(rt, view, st, E.ELLIPSIS, uid)
+    names1 = sorted(e.object_name(rt, int(i)) for i in ids1)
+    names2 = sorted(e.object_name(rt, int(i)) for i in ids2)
+    assert names1 == ["a", "b"] and names2 == ["b"], (names1, names2)
+    e.close()

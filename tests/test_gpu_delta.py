@@ -143,7 +143,7 @@ def test_client_apply_updates_and_consistency():
     ctx = consistency.Context(metadata={})
     object.__setattr__(ctx, "deadline", 0)  # no retries
     ok, err = c.CheckOne(ctx, consistency.Snapshot("3"), founders[2])  # the old revision is gone
-    assert isinstance(err, E.GckError) and err.code == E.GCK_E_REVISION
+    assert isinstance(err, E.GckError) and err.code == E.GCK_E_REVISION_GONE
     c.ApplyUpdates(5, [rel.Update(rel.UpdateDelete, founders[0])])
     assert c.Check(None, consistency.Full(), *founders) == ([False, True, True], None)
     # stale revision, unknown update type, rejected relationship: nothing is applied
