@@ -17,6 +17,7 @@ batch plus further batches of the same generator, ~15 s of CPU work — with eve
 check compared against the GPU's answer (`oracle_agreement`).
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -45,7 +46,10 @@ def parse():
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/pmc_traffic.sh)")
-    ap.add_argument("--host-steps", type=int, default=10, help="PCIe-inclusive host-buffer steps (0 = skip)")
+    ap.add_argument("--host-steps", type=int, default=20, help="PCIe-inclusive host-buffer steps (0 = skip)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="check batches in flight (gck_check_submit on this many streams): the next batch's "
+                         "bundles fill the tail of the previous one; 1 = one batch at a time")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--bundle-checks", type=int, default=0)
     ap.add_argument("--bundle-frontier", type=int, default=0)
@@ -178,7 +182,8 @@ def main():
     t_gen = time.time() - t0
 
     t0 = time.time()
-    eng = Engine(device=local, profile=not args.no_profile,
+    depth = max(1, args.inflight)
+    eng = Engine(device=local, profile=not args.no_profile, workspaces=max(2, depth),
                  max_batch=args.batch * world if args.partitioned else args.batch, wide_only=args.wide_only,
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
@@ -227,15 +232,34 @@ def main():
             eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream,
                                   contexts=CONTEXTS)
     else:
-        items = WL.checks(args.batch, 1000 + rank)
-        perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
-        err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+        # distinct batches, rotated through warm-up and timed steps (no step re-reads a batch a
+        # previous step left in the caches), each with its own result buffers; up to `depth`
+        # of them in flight on as many streams (gck_check_submit / gck_check_wait)
+        n_rot = args.warmup + args.steps
+        rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(n_rot)]
+        outs = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
+                 torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
+        streams = [torch.cuda.Stream(dev) for _ in range(depth)]
+        torch.cuda.synchronize()
+        cursor = {"k": 0}
+        pending = collections.deque()
 
         def step():
-            eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream)
+            k = cursor["k"]
+            cursor["k"] += 1
+            if len(pending) >= depth:
+                pending.popleft().wait()
+            pending.append(eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
+                                      device=True, stream=streams[k % depth].cuda_stream))
+
+        def drain():
+            while pending:
+                pending.popleft().wait()
 
     for _ in range(args.warmup):
         step()
+    if WL.kind != "mixed" and not args.partitioned:
+        drain()
     torch.cuda.synchronize()
     eng.reset_stats()
     if world > 1:
@@ -244,10 +268,14 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if WL.kind != "mixed" and not args.partitioned:
+        drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if WL.kind != "mixed" and not args.partitioned:  # the first timed batch and its results
+        items, (perm, err) = rot[args.warmup], outs[args.warmup]
     st = eng.stats()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -265,18 +293,50 @@ def main():
     errs = err.cpu().numpy()
 
     # ---- PCIe-inclusive rate (host buffers: H2D items + kernels + D2H results), never `value` --
+    # SURVEY §8(d)'s step: the items start in (pageable) host memory and the results end there;
+    # the same rotated batches, `depth` in flight (gck_check_submit with host buffers: each
+    # batch's copies overlap the other batches' kernels), and one at a time for reference.
     host_rate = None
-    if WL.kind == "nested" and not args.partitioned and args.host_steps > 0:
-        h_items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
-        eng.check_bulk(h_items)
-        t0 = time.perf_counter()
-        for _ in range(args.host_steps):
-            hp, he = eng.check_bulk(h_items)
-        dt_h = time.perf_counter() - t0
-        host_rate = {"value": round(args.host_steps * args.batch / dt_h, 1), "unit": "checks/s",
-                     "ms_per_step": round(dt_h / args.host_steps * 1e3, 4),
-                     "same_results": bool((hp == res).all() and (he == errs).all()),
-                     "note": "gck_check_bulk with host buffers (pageable numpy): 20-B items H2D, 1+4 B results D2H"}
+    if WL.kind != "mixed" and not args.partitioned and args.host_steps > 0:
+        h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot]
+        ref0 = (outs[args.warmup][0].cpu().numpy(), outs[args.warmup][1].cpu().numpy())
+        # the same batches in pinned host memory (gck_host_alloc: DMA straight from / into them)
+        p_rot = []
+        for b in h_rot:
+            a = eng.host_array(len(b), ITEM_DTYPE)
+            a[:] = b
+            p_rot.append((a, eng.host_array(len(b), np.uint8), eng.host_array(len(b), np.int32)))
+
+        def host_run(n_batches, dq, pinned):
+            res, q = {}, collections.deque()
+            for j in range(n_batches):
+                k = j % len(h_rot)
+                if len(q) >= dq:
+                    kk, b = q.popleft()
+                    res[kk] = b.wait()
+                q.append((k, eng.submit_into(*p_rot[k]) if pinned else eng.submit(h_rot[k])))
+            while q:
+                kk, b = q.popleft()
+                res[kk] = b.wait()
+            return res
+
+        def timed(dq, pinned):
+            host_run(args.warmup, dq, pinned)
+            t0 = time.perf_counter()
+            r = host_run(args.host_steps, dq, pinned)
+            dt = time.perf_counter() - t0
+            return r, {"value": round(args.host_steps * args.batch / dt, 1),
+                       "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
+        hres, main = timed(depth, True)
+        pres, pageable = timed(depth, False)
+        _, one = timed(1, True)
+        k0 = args.warmup % len(h_rot)
+        same = all(k0 in r and (r[k0][0] == ref0[0]).all() and (r[k0][1] == ref0[1]).all() for r in (hres, pres))
+        host_rate = {**main, "unit": "checks/s", "inflight": depth, "pageable": pageable, "one_at_a_time": one,
+                     "same_results": bool(same),
+                     "note": "gck_check_submit/wait over host buffers, rotated batches: 20-B items H2D by DMA from "
+                             "pinned host memory (gck_host_alloc), kernels, 1+4 B results D2H into pinned host "
+                             "memory; `pageable`: numpy buffers through the engine's pinned staging copies"}
 
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
     prog = tab = None
@@ -290,7 +350,9 @@ def main():
 
         prog, tab = WL.oracle()
         host_items = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    # host threads for the oracle: the box's CPU share (OMP_NUM_THREADS, 16 per GPU there) —
+    # nproc / os.cpu_count() report the whole host, which this process does not own
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
 
     # ---- roofline of the dominant kernels (SURVEY.md §8d algorithmic bytes) -------------------
     # One batch = one k_bundles<1> launch (every check) + one k_bundles<16> launch (the deferred
@@ -302,10 +364,18 @@ def main():
     n_batches = max(1, st["batches"])
     roof = None
     if prog is not None and st["bundle_launches"] and st["bundle_ms"] > 0 and not args.partitioned:
-        if WL.union_only:
-            cnt = corc.count_bfs(prog, tab, host_items, threads=threads)
-        else:  # joins: the recursive oracle's own row / edge counts (memoised per check)
-            cnt = corc.check(prog, tab, host_items, threads=threads)[2]
+        # counted on up to 4 of the rotated timed batches, averaged
+        n_cnt = min(4, args.steps) if WL.kind != "mixed" else 1
+        cnt = collections.Counter()
+        for k in range(n_cnt):
+            hk = (rot[args.warmup + k].cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+                  if WL.kind != "mixed" else host_items)
+            if WL.union_only:
+                ck = corc.count_bfs(prog, tab, hk, threads=threads)
+            else:  # joins: the recursive oracle's own row / edge counts (memoised per check)
+                ck = corc.check(prog, tab, hk, threads=threads)[2]
+            cnt.update(ck)
+        cnt = {k: v / n_cnt for k, v in cnt.items()}
         b_alg = 25 * args.batch + 8 * cnt["rows"] + 4 * cnt["edges"]
         ms_a = st["bundle_ms"] / st["bundle_launches"]
         ms_b = st["giant_ms"] / st["bundle_launches"]
@@ -320,6 +390,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "kernel": "k_bundles<1> + k_bundles<16> (one launch each per batch)",
                 "alg_bytes_per_launch": int(b_alg),
+                # the whole job: algorithmic bytes of every timed batch / the timed region (launches
+                # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)
+                "achieved_job": round(b_alg * args.steps / elapsed / 1e9, 3),
+                "inflight": depth,
                 "alg_counts": {k: int(v) for k, v in cnt.items()},
                 "mean_launch_ms": {"k_bundles<1>": round(ms_a, 4), "k_bundles<16>": round(ms_b, 4)},
                 "traffic_source": traffic_src,
@@ -336,7 +410,11 @@ def main():
         corc.check(prog, tab, host_items, threads=threads)
         per_batch = time.perf_counter() - t0
         extra = int(max(0, min(args.cpu_max_batches, args.cpu_seconds / max(per_batch, 1e-6))) - 1)
-        batches = [(items, perm.clone(), err.clone())]
+        # the timed batches with the results the timed region produced, then further batches
+        timed = list(range(args.warmup, args.warmup + args.steps)) if WL.kind != "mixed" else []
+        batches = ([(rot[k], outs[k][0], outs[k][1]) for k in timed[:extra + 1]] if timed
+                   else [(items, perm.clone(), err.clone())])
+        extra = max(0, extra + 1 - len(batches))
         for k in range(extra):
             it = WL.checks(args.batch, 5000 + k)
             pk = torch.zeros_like(perm)
@@ -368,9 +446,10 @@ def main():
                                             "oracle": [int(cp[i]), int(ce[i])]} for i in bad[:3]]})
         agree = n_ok / n_s
         cpu = {"value": round(n_s / dt, 1), "unit": "checks/s", "cores": threads, "kind": "port",
-               "sample": f"{len(host)} batches x {args.batch} checks (the timed batch + seeds 5000..), same "
-                         f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads), "
-                         f"{dt:.1f}s; every sampled check compared with the GPU result"}
+               "sample": f"{len(host)} batches x {args.batch} checks (the timed batches, then seeds 5000..), same "
+                         f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads "
+                         f"= the box's CPU share; nproc reports {os.cpu_count()}), {dt:.1f}s; every sampled check "
+                         f"compared with the GPU result"}
 
     if rank == 0 and WL.kind == "mixed" and not args.no_oracle:
         agree = agree_mixed
@@ -398,7 +477,8 @@ def main():
             **({"disagreements": disagree} if disagree else {}),
             "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),
                            "COND": int((res == 3).sum()), "ERR": int((errs != 0).sum())},
-            "engine": {"levels_per_batch": round(st["levels"] / n_batches, 1),
+            "engine": {"levels_per_bundle": round(st["levels"] / max(1, st["bundles"]), 2),
+                       "bundles_per_batch": round(st["bundles"] / n_batches, 1),
                        "entries_per_batch": int(st["entries_expanded"] / n_batches),
                        "edges_per_batch": int(st["edges_enumerated"] / n_batches),
                        "probes_per_batch": int(st["membership_probes"] / n_batches),

@@ -110,6 +110,8 @@ struct Workspace {
   int32_t* b_derr = nullptr;
   uint8_t* b_hperm = nullptr; // host batch: the caller's result buffers (copied out by the wait)
   int32_t* b_herr = nullptr;
+  uint8_t* b_xperm = nullptr; // host batch: where the results' D2H lands — the pinned staging, or
+  int32_t* b_xerr = nullptr;  // the caller's buffers themselves when they are gck_host_alloc memory
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
   unsigned b_seq = 0;         // publish sequence of stage A
   float b_ms = 0.f;
@@ -1585,6 +1587,8 @@ static void add_counters(Engine& e, const DevCounters& h) {
   e.stats.edges_enumerated += h.edges;
   e.stats.ext_edges += h.ext_edges;
   e.stats.bidir_checks += h.bidir;
+  e.stats.levels += h.bundle_levels;
+  e.stats.bundles += h.bundles;
 }
 
 // Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
@@ -1794,8 +1798,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(w.ev1, st));
   if (host_out) {
-    HIP_OK(hipMemcpyAsync(w.h_perm, d_perm, n, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(w.h_err, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
   publish_launch(w, st);
 }
@@ -1886,9 +1890,9 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
                        d_err);
     HIP_OK(hipGetLastError());
   }
-  if (host_out) {  // the deferred checks' results, in place in the staging
-    HIP_OK(hipMemcpyAsync(w.h_perm, d_perm, n, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(w.h_err, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  if (host_out) {  // the deferred checks' results, in place
+    HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
   HIP_OK(hipStreamSynchronize(st));
   return ms;
@@ -1962,6 +1966,42 @@ static void stage_caveats(Workspace& w, const std::vector<uint8_t>& table, uint3
 // the pinned staging). The synchronous entry points are the two back to back; gck_check_submit /
 // gck_check_wait expose them separately so that the next batch is queued while this one runs.
 
+// Is [p, p + bytes) inside one pinned host buffer of this engine (gck_host_alloc)?
+static bool host_pinned(Engine& e, const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(e.host_mu);
+  if (e.host_bufs.empty()) return false;
+  const uintptr_t a = (uintptr_t)p;
+  auto it = e.host_bufs.upper_bound(a);
+  if (it == e.host_bufs.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+
+void* host_alloc(Engine& e, size_t bytes) {
+  HIP_OK(hipSetDevice(e.cfg.device));
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+  std::lock_guard<std::mutex> lk(e.host_mu);
+  e.host_bufs[(uintptr_t)p] = bytes;
+  return p;
+}
+
+void host_free(Engine& e, void* p) {
+  {
+    std::lock_guard<std::mutex> lk(e.host_mu);
+    auto it = e.host_bufs.find((uintptr_t)p);
+    if (it == e.host_bufs.end()) throw Error(GCK_E_INVALID_ARGUMENT, "not a gck_host_alloc buffer of this engine");
+    e.host_bufs.erase(it);
+  }
+  HIP_OK(hipHostFree(p));
+}
+
+void host_free_all(Engine& e) {
+  std::lock_guard<std::mutex> lk(e.host_mu);
+  for (auto& kv : e.host_bufs) (void)hipHostFree(reinterpret_cast<void*>(kv.first));
+  e.host_bufs.clear();
+}
+
 static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_t n, int64_t now_us, uint8_t* perm,
                          int32_t* err, hipStream_t st, bool host) {
   w.b_n = n;
@@ -1976,9 +2016,17 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   w.fail_code = 0;
   w.fail_msg.clear();
   if (host) {
-    // the caller's (pageable) items through the pinned staging: one host copy, one DMA
-    std::memcpy(w.h_items, items, (size_t)n * sizeof(gck_item));
-    HIP_OK(hipMemcpyAsync(w.d_items, w.h_items, (size_t)n * sizeof(gck_item), hipMemcpyHostToDevice, w.b_st));
+    // items: a DMA straight from the caller's buffer when it is pinned (gck_host_alloc), else
+    // through the workspace's pinned staging (one host copy, one DMA); results likewise
+    if (host_pinned(e, items, (size_t)n * sizeof(gck_item))) {
+      HIP_OK(hipMemcpyAsync(w.d_items, items, (size_t)n * sizeof(gck_item), hipMemcpyHostToDevice, w.b_st));
+    } else {
+      std::memcpy(w.h_items, items, (size_t)n * sizeof(gck_item));
+      HIP_OK(hipMemcpyAsync(w.d_items, w.h_items, (size_t)n * sizeof(gck_item), hipMemcpyHostToDevice, w.b_st));
+    }
+    const bool pin_out = host_pinned(e, perm, n) && host_pinned(e, err, (size_t)n * 4);
+    w.b_xperm = pin_out ? perm : w.h_perm;
+    w.b_xerr = pin_out ? err : w.h_err;
   }
   if (e.cfg.flags & GCK_FLAG_NO_BUNDLE) {
     w.b_bundles = false;
@@ -1999,15 +2047,15 @@ static void finish_batch(Engine& e, Workspace& w) {
   } else {
     check_range_wide(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, &w.b_ms);
     if (w.b_hperm) {
-      HIP_OK(hipMemcpyAsync(w.h_perm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, w.b_st));
-      HIP_OK(hipMemcpyAsync(w.h_err, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, w.b_st));
+      HIP_OK(hipMemcpyAsync(w.b_xperm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, w.b_st));
+      HIP_OK(hipMemcpyAsync(w.b_xerr, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, w.b_st));
       HIP_OK(hipStreamSynchronize(w.b_st));
     }
   }
 }
 
 static void copy_out(Workspace& w) {
-  if (!w.b_hperm) return;
+  if (!w.b_hperm || w.b_xperm != w.h_perm) return;  // device batch, or results DMA'd in place
   std::memcpy(w.b_hperm, w.h_perm, w.b_n);
   std::memcpy(w.b_herr, w.h_err, (size_t)w.b_n * 4);
 }

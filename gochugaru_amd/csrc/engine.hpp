@@ -2,6 +2,7 @@
 // device-resident snapshot + workspace. Everything behind the C ABI in include/gck.h.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <condition_variable>
 #include <mutex>
@@ -171,6 +172,8 @@ struct Engine {
   Workspace* part_ws = nullptr;   // the partitioned batch's own workspace (partition.inc)
   uint64_t part_generation = 0;   // the snapshot generation a partitioned batch started on
   std::mutex stats_mu;            // stats are added by concurrent batches
+  std::mutex host_mu;             // pinned host buffers handed out by gck_host_alloc (base -> bytes)
+  std::map<uintptr_t, size_t> host_bufs;
   uint64_t generation = 0;        // bumped by every device snapshot (commit, Watch batch)
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
@@ -226,6 +229,11 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
                    int32_t* err, void* stream, bool host, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
 void device_wait(Engine& e, Workspace* w);
+// Pinned host buffers (gck_host_alloc): a host batch whose items / results live in one is
+// copied by DMA directly, without the workspace's staging copy.
+void* host_alloc(Engine& e, size_t bytes);
+void host_free(Engine& e, void* p);
+void host_free_all(Engine& e);
 // Finishes every batch in flight (a writer holding the engine exclusively calls this before
 // it replaces the snapshot: the batches keep the results of the snapshot they started on).
 void drain_batches(Engine& e);

@@ -14,7 +14,10 @@ thread_local std::string g_last_error;
     if (!(cond)) throw Error(code, msg); \
   } while (0)
 
-Engine::~Engine() { device_free(*this); }
+Engine::~Engine() {
+  device_free(*this);
+  host_free_all(*this);
+}
 
 void reset_caveats(Engine& e) {
   e.caveat_instances.assign(1, {"", ""});
@@ -123,7 +126,7 @@ static Schema& need_schema(Engine& e) {
 extern "C" {
 
 static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
-static_assert(sizeof(gck_stats) == 176, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
+static_assert(sizeof(gck_stats) == 184, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32 && sizeof(gck_update) == 40, "item/tuple/update layout");
 
 int gck_abi_version(void) { return GCK_ABI_VERSION; }
@@ -645,6 +648,21 @@ int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* 
     }
     b->w = w;
     *out = b;
+  });
+}
+
+int gck_host_alloc(gck_engine* ge, size_t bytes, void** out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = host_alloc(e, bytes);
+  });
+}
+
+int gck_host_free(gck_engine* ge, void* p) {
+  return guard([&] {
+    Engine& e = need(ge);
+    if (p) host_free(e, p);
   });
 }
 

@@ -190,6 +190,8 @@ struct DevCounters {  // device-side counters, reset per level where noted
   unsigned long long ext_edges;
   unsigned long long expanded;
   unsigned long long bidir;         // checks evaluated bidirectionally
+  unsigned long long bundle_levels; // BFS levels run by bundles (summed over bundles)
+  unsigned long long bundles;       // bundles run
 };
 
 }  // namespace gck

@@ -15,7 +15,8 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgck.so")
+# GCK_LIBRARY: an instrumented build of the same sources (make TIMING=1 -> libgck_timing.so)
+_LIB_PATH = os.environ.get("GCK_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgck.so")
 
 # ---- constants mirrored from include/gck.h ------------------------------------------------
 GCK_OK = 0
@@ -116,7 +117,7 @@ class _Stats(C.Structure):
                 ("edges_launches", C.c_uint64), ("bundle_ms", C.c_double),
                 ("bundle_launches", C.c_uint64), ("deferred", C.c_uint64),
                 ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64),
-                ("bidir_checks", C.c_uint64)]
+                ("bidir_checks", C.c_uint64), ("bundles", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -165,6 +166,8 @@ _SIGS = {
                                    C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P, C.c_uint32, _P,
                                    C.POINTER(_P)]),
     "gck_check_wait": (C.c_int, [_P, _P]),
+    "gck_host_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    "gck_host_free": (C.c_int, [_P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
     "gck_lookup_resources": (C.c_int, [_P, C.POINTER(_Consistency), C.c_uint16, C.c_uint16, C.c_uint16,
                                        C.c_uint16, C.c_uint32, C.c_int64, _P, _P, C.c_size_t,
@@ -464,6 +467,29 @@ class Engine:
         n = len(items)
         perm = np.zeros(n, dtype=np.uint8)
         err = np.zeros(n, dtype=np.int32)
+        _check(self._lib.gck_check_submit(self._h, C.byref(cs), items.ctypes.data if n else None, n, ctx_arr,
+                                          ctx_lens, n_ctx, now_us, perm.ctypes.data if n else None,
+                                          err.ctypes.data if n else None, 0, None, C.byref(h)))
+        return Batch(self, h, perm, err, items)
+
+    def host_array(self, n: int, dtype) -> np.ndarray:
+        """A numpy array in pinned host memory (gck_host_alloc): host batches over such arrays
+        are copied by DMA directly. Freed with the engine."""
+        dtype = np.dtype(dtype)
+        p = _P()
+        _check(self._lib.gck_host_alloc(self._h, max(1, n * dtype.itemsize), C.byref(p)))
+        buf = (C.c_char * max(1, n * dtype.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dtype, count=n)
+
+    def submit_into(self, items: np.ndarray, perm: np.ndarray, err: np.ndarray,
+                    requirement: int = CONSISTENCY_MIN_LATENCY, revision: int = 0, now_us: int = 0,
+                    contexts: Optional[Sequence] = None) -> "Batch":
+        """A host batch writing its results into caller-provided arrays (pinned ones from
+        host_array() skip the engine's staging copies)."""
+        cs = _Consistency(requirement, 0, revision)
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        h = _P()
+        n = len(items)
         _check(self._lib.gck_check_submit(self._h, C.byref(cs), items.ctypes.data if n else None, n, ctx_arr,
                                           ctx_lens, n_ctx, now_us, perm.ctypes.data if n else None,
                                           err.ctypes.data if n else None, 0, None, C.byref(h)))

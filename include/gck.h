@@ -175,7 +175,7 @@ typedef struct gck_consistency {
 
 typedef struct gck_stats {
   uint64_t batches;
-  uint64_t levels;             /* BFS levels (dispatch waves) executed */
+  uint64_t levels;             /* BFS levels executed: grid-wide levels + every bundle's levels */
   uint64_t entries_expanded;   /* (query, object, node) entries expanded */
   uint64_t row_lookups;        /* CSR rows opened (each = one 8-B offset pair) */
   uint64_t membership_probes;  /* 4-B neighbour reads by membership binary searches */
@@ -196,6 +196,8 @@ typedef struct gck_stats {
   double giant_ms;             /* GCK_FLAG_PROFILE: summed workgroup-bundle kernel time */
   uint64_t deferred_wide;      /* checks handed from workgroup bundles to the grid-wide path */
   uint64_t bidir_checks;       /* checks evaluated bidirectionally (forward + reverse frontier) */
+  uint64_t bundles;            /* check bundles run by the bundle kernels (`levels` also sums
+                                  their BFS levels) */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
@@ -315,6 +317,11 @@ int gck_check_submit(gck_engine* e, const gck_consistency* cs, const gck_item* i
                      int64_t now_us, uint8_t* out_perm, int32_t* out_err, uint32_t flags, void* stream,
                      gck_batch** out);
 int gck_check_wait(gck_engine* e, gck_batch* batch);
+/* Pinned host memory for request / result buffers: a host batch (gck_check_bulk*,
+ * gck_check_submit) whose items or results lie in such a buffer is copied over PCIe by DMA
+ * directly, skipping the engine's own staging copy. Freed with gck_host_free (or gck_destroy). */
+int gck_host_alloc(gck_engine* e, size_t bytes, void** out);
+int gck_host_free(gck_engine* e, void* p);
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
 

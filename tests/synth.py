@@ -17,7 +17,8 @@ Generator (all vectorised in torch, on the GPU for the 1B case):
   sorted random subset of a random window of the user id space (strictly increasing gaps);
 * docs: 1-3 viewer groups each, uniform over all groups;
 * checks: ``doc#view@user``, half sampled from positive reachable pairs (doc -> viewer group
-  -> up to 3 random descents -> a random member), half uniform (doc, user) pairs.
+  -> 0..24 random descents, uniform, stopping at a leaf group -> a random member), half uniform
+  (doc, user) pairs: positive answers come from every depth of the DAG, down to 24 group hops.
 
 Returns CSR arrays in the engine's id space (types user=0, group=1, doc=2; relations
 member=0, viewer=1, view=2) — the same arrays feed the HIP engine (``gck_load_csr``) and the
@@ -176,7 +177,7 @@ def build(target_tuples: float = 1e9, seed: int = 20251003, device="cuda", layer
 
 
 def checks(G: Graph, n: int = 65536, seed: int = 7, positive_frac: float = 0.5,
-           max_descend: int = 3) -> torch.Tensor:
+           max_descend: int = 24) -> torch.Tensor:
     """Check items (gck_item records, 20 B each) as a uint8 tensor [n, 20] on G's device."""
     dev = G.viewer_nbr.device
     gen = _gen(dev, seed)

@@ -225,3 +225,27 @@ def test_lookup_sees_expiration_between_calls():
     names2 = sorted(e.object_name(rt, int(i)) for i in ids2)
     assert names1 == ["a", "b"] and names2 == ["b"], (names1, names2)
     e.close()
+
+
+def test_pinned_host_buffers():
+    """gck_host_alloc buffers: the batch is copied by DMA straight from / into them (no staging
+    copy); results equal the pageable path and the oracle, also when stage B/C run."""
+    schema, tuples, checks = gen.gdocs_deep(2)
+    want = _want(schema, tuples, checks)
+    for kw in ({}, {"bundle_budget": 2}):
+        e = _engine(schema, tuples, workspaces=2, **kw)
+        items = e.make_items([parse_check(c) for c in checks])
+        p_items = e.host_array(len(items), E.ITEM_DTYPE)
+        p_items[:] = items
+        perm, err = e.host_array(len(items), np.uint8), e.host_array(len(items), np.int32)
+        b = e.submit_into(p_items, perm, err, now_us=gen.NOW_US)
+        b.wait()
+        assert _got(perm, err) == want
+        # pinned items, pageable results (and the other way round)
+        perm2, err2 = np.zeros(len(items), np.uint8), np.zeros(len(items), np.int32)
+        e.submit_into(p_items, perm2, err2, now_us=gen.NOW_US).wait()
+        assert _got(perm2, err2) == want
+        perm[:] = 0
+        e.submit_into(items.copy(), perm, err, now_us=gen.NOW_US).wait()
+        assert _got(perm, err) == want
+        e.close()
