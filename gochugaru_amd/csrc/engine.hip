@@ -57,6 +57,7 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
   const uint32_t* src;
   uint64_t src_edges;
   DevCSR d;
+  uint32_t* sig = nullptr;  // ancestor closure: 256-bit signature per row (closure.inc)
 };
 
 struct DeviceSnapshot {
@@ -80,6 +81,10 @@ struct DeviceSnapshot {
   uint32_t n_nodes = 0, n_items = 0, n_csrs = 0, n_types = 0, n_rels = 0;
   uint32_t n_fwd = 0;      // forward nodes; [n_fwd, n_nodes) is the reverse program (bidir.inc)
   bool has_bidir = false;  // some forward node is NF_BIDIR
+  // closure-join stage (closure.inc): the flat table of eligible roots (in the program block)
+  std::vector<unsigned char> cj_host;
+  uint32_t cj_n_desc = 0, cj_o_meta = 0, cj_o_entries = 0;
+  const unsigned char* d_cj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
   uint8_t* cav_static = nullptr;  // per caveat instance (Engine::caveat_static)
@@ -146,7 +151,9 @@ struct Workspace {
   unsigned long long* b_vis = nullptr;
   uint32_t* b_vlog = nullptr;  // per slot: claimed visited slots (cleared by the bundle)
   uint32_t* b_deferred = nullptr;
-  unsigned* b_ctrs = nullptr;      // [0] bundle ctr, [1] deferred, [2] giant bundle ctr, [3] deferred2
+  uint32_t* c_deferred = nullptr;  // checks the closure-join stage left to the bundles
+  unsigned* b_ctrs = nullptr;      // kBCtrs words: [0] bundle ctr, [1] deferred, [2] giant bundle ctr,
+                                   // [3] deferred2, [4] closure-join deferred (closure.inc)
   unsigned* h_bctrs = nullptr;     // pinned
   uint32_t b_budget = 1024;
   // giant-check stage: one 16-wave workgroup per bundle (allocated on first use: ensure_giant)
@@ -972,6 +979,7 @@ __global__ void __launch_bounds__(kBlock) k_final(const DevQuery* __restrict__ q
 }
 
 constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kBCtrs = 8;  // per-batch stage counters after DevCounters (Workspace::b_ctrs)
 
 #include "bundle.inc"
 
@@ -1205,6 +1213,7 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 }
 
 #include "heights.inc"
+#include "closure.inc"
 #include "bidir.inc"
 
 // Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
@@ -1334,6 +1343,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     const size_t o_counts = put(counts.data(), counts.size() * 4);
     const size_t o_cst = put(cst.data(), cst.size());
     const size_t o_crow = put(crow.data(), crow.size() * 4);
+    const size_t o_cj = ds->cj_host.empty() ? 0 : put(ds->cj_host.data(), ds->cj_host.size());
     std::vector<unsigned long long> hp(ds->hgt.size());  // heights array of each forward node
     for (size_t n = 0; n < hp.size(); ++n) hp[n] = (unsigned long long)(uintptr_t)ds->hgt[n];
     const size_t o_hgt = put(hp.data(), hp.size() * 8);
@@ -1346,6 +1356,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     ds->cav_static = d_blob + o_cst;
     ds->cav_row = reinterpret_cast<uint32_t*>(d_blob + o_crow);
     ds->d_hgt = reinterpret_cast<const unsigned long long*>(d_blob + o_hgt);
+    ds->d_cj = ds->cj_host.empty() ? nullptr : d_blob + o_cj;
     ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
     if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
     ds->q_bits = 31 - ds->node_bits;
@@ -1418,15 +1429,15 @@ static Workspace* create_workspace(Engine& e) {
     // the level / batch counters and the bundle counters share one buffer (one memset, one copy
     // back per batch)
     static_assert(sizeof(DevCounters) % 8 == 0, "bundle counters follow DevCounters");
-    w->ctr = reinterpret_cast<DevCounters*>(dalloc<unsigned char>(w->allocs, sizeof(DevCounters) + 4 * sizeof(unsigned)));
+    w->ctr = reinterpret_cast<DevCounters*>(dalloc<unsigned char>(w->allocs, sizeof(DevCounters) + kBCtrs * sizeof(unsigned)));
     w->b_ctrs = reinterpret_cast<unsigned*>(w->ctr + 1);
     w->d_items = dalloc<gck_item>(w->allocs, w->max_batch);
     w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
     w->d_err = dalloc<int32_t>(w->allocs, w->max_batch);
-    HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters) + 8 * sizeof(unsigned),
+    HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters) + (kBCtrs + 4) * sizeof(unsigned),
                          hipHostMallocCoherent | hipHostMallocMapped));
     w->h_bctrs = reinterpret_cast<unsigned*>(w->h_ctr + 1);
-    w->h_seq = w->h_bctrs + 4;
+    w->h_seq = w->h_bctrs + kBCtrs;
     *w->h_seq = 0;
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&w->d_hpub), w->h_ctr, 0));
     // pinned staging of host batches: 20 B of items in, 5 B of results out per check
@@ -1453,6 +1464,7 @@ static Workspace* create_workspace(Engine& e) {
       w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots);
       HIP_OK(hipMemsetAsync(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long), nullptr));
       w->b_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
+      w->c_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
       w->b_budget = cf.bundle_budget ? cf.bundle_budget : 1024;
       w->g_fc = cf.giant_frontier ? cf.giant_frontier : 65536;
       w->g_vslots = 1u << ceil_log2(cf.giant_visited ? cf.giant_visited : 262144);
@@ -1462,7 +1474,7 @@ static Workspace* create_workspace(Engine& e) {
       w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
       w->def_err = dalloc<int32_t>(w->allocs, w->max_batch);
     }
-    HIP_OK(hipMemsetAsync(w->ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), nullptr));
+    HIP_OK(hipMemsetAsync(w->ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), nullptr));
     w->ctr_clean = true;
     HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&w->ev0));
@@ -1589,6 +1601,7 @@ static void add_counters(Engine& e, const DevCounters& h) {
   e.stats.bidir_checks += h.bidir;
   e.stats.levels += h.bundle_levels;
   e.stats.bundles += h.bundles;
+  e.stats.closure_checks += h.closure;
 }
 
 // Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
@@ -1600,7 +1613,7 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   c.ck_items = d_items;
   HIP_OK(hipEventRecord(w.ev0, st));
   w.ctr_clean = false;
-  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));
+  HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));
   HIP_OK(hipMemsetAsync(w.visited, 0xFF, w.visited_cap * sizeof(unsigned long long), st));
   DevCounters init{};
   init.n_queries = n;
@@ -1716,7 +1729,7 @@ static void elapsed_ms(float* out, hipEvent_t a, hipEvent_t b) {
   HIP_OK(r);
 }
 
-constexpr uint32_t kPubWords = (sizeof(DevCounters) + 4 * sizeof(unsigned)) / 4;
+constexpr uint32_t kPubWords = (sizeof(DevCounters) + kBCtrs * sizeof(unsigned)) / 4;
 
 static void publish_launch(Workspace& w, hipStream_t st) {
   const unsigned seq = ++w.pub_seq;
@@ -1779,11 +1792,34 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
   if (timing_env) HIP_OK(hipMemsetAsync(w.timing, 0, w.timing_cap * 8, st));
-  if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + 4 * sizeof(unsigned), st));  // + b_ctrs
+  if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));  // + b_ctrs
   w.ctr_clean = false;
   // one event opens the batch and stage A, one closes stage A: every record is a host API call
   // on the per-batch path
   HIP_OK(hipEventRecord(w.ev0, st));
+  // the closure-join stage answers the nested-group checks it can (closure.inc); the bundle
+  // kernel then takes what it left, reading the count on the device
+  const DeviceSnapshot& ds = *e.dev;
+  if (ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE)) {
+    CjArgs j{};
+    j.items = d_items;
+    j.n = n;
+    j.out_perm = d_perm;
+    j.out_err = d_err;
+    j.deferred = w.c_deferred;
+    j.n_deferred = w.b_ctrs + 4;
+    j.table = ds.d_cj;
+    j.n_fwd = ds.n_fwd;
+    j.n_desc = ds.cj_n_desc;
+    j.n_types = ds.n_types;
+    j.table_bytes = (uint32_t)((ds.cj_host.size() + 3) & ~(size_t)3);
+    j.o_meta = ds.cj_o_meta;
+    j.o_entries = ds.cj_o_entries;
+    hipLaunchKernelGGL(k_closure_join, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
+    HIP_OK(hipGetLastError());
+    a.idx = w.c_deferred;
+    a.n_dev = w.b_ctrs + 4;
+  }
   const bool prog_lds = program_in_lds(c);
   // bidirectional instantiation only when the snapshot has an eligible permission (bidir.inc)
   const bool bd = e.dev->has_bidir;

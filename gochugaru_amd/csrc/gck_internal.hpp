@@ -192,6 +192,7 @@ struct DevCounters {  // device-side counters, reset per level where noted
   unsigned long long bidir;         // checks evaluated bidirectionally
   unsigned long long bundle_levels; // BFS levels run by bundles (summed over bundles)
   unsigned long long bundles;       // bundles run
+  unsigned long long closure;       // checks answered by the closure-join stage (closure.inc)
 };
 
 }  // namespace gck

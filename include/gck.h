@@ -106,6 +106,8 @@ extern "C" {
 #define GCK_FLAG_NO_MHASH 4u     /* gck_config.flags: no hashed membership index (binary search) */
 #define GCK_FLAG_NO_GIANT 8u     /* gck_config.flags: deferred checks skip the workgroup-bundle stage */
 #define GCK_FLAG_NO_BIDIR 16u    /* gck_config.flags: forward-only search (no bidirectional checks) */
+#define GCK_FLAG_NO_CLOSURE 32u  /* gck_config.flags: no closure-join stage (nested-group checks take
+                                    the bundle search) */
 
 typedef struct gck_engine gck_engine;
 
@@ -198,6 +200,7 @@ typedef struct gck_stats {
   uint64_t bidir_checks;       /* checks evaluated bidirectionally (forward + reverse frontier) */
   uint64_t bundles;            /* check bundles run by the bundle kernels (`levels` also sums
                                   their BFS levels) */
+  uint64_t closure_checks;     /* checks answered by the closure-join stage (nested groups) */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

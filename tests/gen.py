@@ -243,6 +243,14 @@ def nested(seed, n_users=200, n_groups=120, layers=8, n_docs=80):
         for _ in range(rng.randint(1, 3)):
             t.append(f"doc:d{d}#viewer@group:g{_pick(rng, per * 2)}#member")
     checks = [f"doc:d{_pick(rng, n_docs)}#view@user:u{_pick(rng, n_users)}" for _ in range(400)]
+    # the closure-join shapes besides doc#view@user: a group's own members, userset subjects,
+    # subjects of an unlisted type (left to the bundles), unknown objects
+    checks += [f"group:g{_pick(rng, n_groups)}#member@user:u{_pick(rng, n_users)}" for _ in range(60)]
+    checks += [f"doc:d{_pick(rng, n_docs)}#view@group:g{_pick(rng, n_groups)}#member" for _ in range(40)]
+    checks += [f"group:g{_pick(rng, n_groups)}#member@group:g{_pick(rng, n_groups)}#member" for _ in range(30)]
+    checks += [f"doc:d{_pick(rng, n_docs)}#viewer@group:g{_pick(rng, n_groups)}#member" for _ in range(20)]
+    checks += [f"doc:d{_pick(rng, n_docs + 5)}#view@user:u{_pick(rng, n_users + 5)}" for _ in range(20)]
+    checks += [f"doc:d{_pick(rng, n_docs)}#view@doc:d{_pick(rng, n_docs)}" for _ in range(5)]
     return NESTED, t, checks
 
 

@@ -166,30 +166,35 @@ def test_semantics_caveats():
 # ---- random graphs vs the oracle -------------------------------------------------------------
 
 PATHS = {
-    # persistent wave-bundle kernel (default)
+    # closure-join stage, then the persistent wave-bundle kernel (default)
     "bundle": {},
     # grid-wide level-synchronous kernels only
     "wide": {"wide_only": True},
+    # the bundle machinery on its own (no closure-join stage) ...
+    "noclosure": {"closure": False},
     # tiny per-wave scratch: most bundles overflow and are re-run by the later stages
-    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 8},
+    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 8, "closure": False},
     # tiny work budget: almost every check is handed to a 16-wave workgroup bundle
-    "giant": {"bundle_budget": 2},
+    "giant": {"bundle_budget": 2, "closure": False},
     # ... and those overflow their workgroup scratch into the grid-wide path
-    "giant-deferred": {"bundle_budget": 2, "giant_frontier": 8, "giant_visited": 16, "giant_slots": 3},
+    "giant-deferred": {"bundle_budget": 2, "giant_frontier": 8, "giant_visited": 16, "giant_slots": 3,
+                       "closure": False},
     # deferred checks straight to the grid-wide path
-    "giant-skip": {"bundle_budget": 2, "giant_stage": False},
+    "giant-skip": {"bundle_budget": 2, "giant_stage": False, "closure": False},
+    # what the closure-join stage leaves goes through the bundles' deferral chain
+    "closure-giant": {"bundle_budget": 2},
     # one check per wavefront, few resident waves
-    "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4},
+    "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4, "closure": False},
     # binary-search membership instead of the hashed index, both paths
     "nohash": {"membership_hash": False},
     "nohash-wide": {"membership_hash": False, "wide_only": True},
-    # forward-only wave bundles (no bidirectional checks)
+    # forward-only wave bundles (no bidirectional checks, hence no closure join)
     "nobidir": {"bidir": False},
     # bidirectional checks always expanding only the smaller side (most carrying) ...
-    "bidir-one": {"bidir_both": 1},
+    "bidir-one": {"bidir_both": 1, "closure": False},
     # ... or always both sides; and bidirectional checks deferred to the later stages
-    "bidir-all": {"bidir_both": 1 << 30},
-    "bidir-deferred": {"bundle_budget": 6, "bundle_frontier": 16, "bundle_visited": 64},
+    "bidir-all": {"bidir_both": 1 << 30, "closure": False},
+    "bidir-deferred": {"bundle_budget": 6, "bundle_frontier": 16, "bundle_visited": 64, "closure": False},
 }
 
 
@@ -212,7 +217,9 @@ def test_random_parity(family, seed, path):
     if path == "bundle" and not deep:
         assert e.stats()["deferred"] == 0
     if path == "bundle" and family in ("nested", "gdocs_deep"):
-        assert e.stats()["bidir_checks"] > 0
+        assert e.stats()["closure_checks"] > 0  # nested doc#view / group#member checks
+    if path == "noclosure" and family in ("nested", "gdocs_deep"):
+        assert e.stats()["bidir_checks"] > 0 and e.stats()["closure_checks"] == 0
     if path in ("nobidir", "wide") or family == "caveated":
         assert e.stats()["bidir_checks"] == 0
     e.close()
