@@ -1,0 +1,74 @@
+"""Throughput of config-4 device batches vs batches in flight, repeated in one process (variance
+check): python tools/inflight_probe.py [--tuples 1e9] [--reps 3] [--batches 400]."""
+import argparse
+import collections
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tuples", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batches", type=int, default=400)
+    ap.add_argument("--depths", default="1,2,3,4,6,8")
+    ap.add_argument("--closure", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    from gochugaru_amd.engine import Engine
+    from tests import synth
+    dev = torch.device("cuda", 0)
+    G = synth.build(args.tuples, device=dev)
+    depths = [int(x) for x in args.depths.split(",")]
+    eng = Engine(device=0, workspaces=max(depths), closure=bool(args.closure))
+    eng.load_schema(synth.SCHEMA)
+    eng.reserve_objects(synth.T_USER, G.n_users)
+    eng.reserve_objects(synth.T_GROUP, G.n_groups)
+    eng.reserve_objects(synth.T_DOC, G.n_docs)
+    eng.begin_snapshot(1)
+    keep = []
+    for rel, st, sr, n_rows, off, nbr in G.csrs():
+        off32 = off.to(torch.int32).contiguous()
+        keep.append((off32, nbr))
+        eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr.data_ptr(), nbr.numel(), device=True)
+    torch.cuda.synchronize()
+    eng.commit_snapshot()
+    n = 65536
+    rot = [synth.checks(G, n, seed=3000 + k) for k in range(64)]
+    outs = [(torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.int32, device=dev))
+            for _ in range(64)]
+    streams = [torch.cuda.Stream(dev) for _ in range(max(depths))]
+    torch.cuda.synchronize()
+
+    def run(depth, nb):
+        q = collections.deque()
+        for k in range(nb):
+            if len(q) >= depth:
+                q.popleft().wait()
+            j = k % 64
+            q.append(eng.submit(rot[j].data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), device=True,
+                                stream=streams[k % depth].cuda_stream))
+        while q:
+            q.popleft().wait()
+
+    for r in range(args.reps):
+        for d in depths:
+            run(d, 20)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(d, args.batches)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"rep {r} inflight {d}: {args.batches * n / dt / 1e6:8.1f} M checks/s  {dt / args.batches * 1e3:.4f} ms/batch",
+                  flush=True)
+    st = eng.stats()
+    print("closure_checks", st["closure_checks"], "bundles", st["bundles"])
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,23 @@
+# Round-2 profile set (run on the GPU box, binaries built beforehand in this container):
+#   bash tools/pmc_r02.sh <out dir under gpurun_out> [bench args]
+# 1. FETCH_SIZE / WRITE_SIZE calibration on known byte counts (tools/gather_probe)
+# 2. rocprofv3 kernel trace + stats of the default bench command
+# 3. FETCH_SIZE and WRITE_SIZE passes (separate runs) over a short bench command
+set -e
+OUT=${1:-gpurun_out/pmc}
+shift || true
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p "$OUT"
+GP=tools/gather_probe/gather_probe
+timeout -k 10 120 $GP > "$OUT/gather_plain.jsonl"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/gfetch" -o gfetch --output-format csv -- $GP > "$OUT/gather_fetch.jsonl" 2> "$OUT/gather_fetch.err"
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/gwrite" -o gwrite --output-format csv -- $GP > "$OUT/gather_write.jsonl" 2> "$OUT/gather_write.err"
+echo "calibration done"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
+echo "kernel trace done"
+SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --host-steps 0 $*"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- $SHORT > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- $SHORT > "$OUT/write.json" 2> "$OUT/write.err"
+echo "pmc done"
+python3 tools/traffic_summary.py "$OUT" > "$OUT/traffic.json"
+cat "$OUT/traffic.json"

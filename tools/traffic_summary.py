@@ -1,8 +1,10 @@
-"""Per-batch HBM bytes of the bundle kernels from tools/pmc_traffic.sh output.
+"""Per-batch HBM bytes of the check kernels, from tools/pmc_r02.sh output.
 
-FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived counters). On gfx950
-FETCH_SIZE reports half the bytes of wide reads (MI355X_MICROARCH.md §HBM), so it is doubled;
-for this kernel's narrow random reads the factor is uncalibrated (the raw values are kept)."""
+FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived counters). MI355X_MICROARCH.md
+§HBM establishes FETCH_SIZE = 1/2 of the bytes for wide streaming reads only; tools/gather_probe
+measures the factor for random aligned reads of 4, 16, 32 and 64 B from a table far larger than the
+Infinity Cache (known bytes), and the per-batch figure is corrected with the factor of the access
+width that dominates the stage-A kernels' reads (the 32-B signature and 64-B index reads)."""
 import csv
 import glob
 import json
@@ -10,24 +12,72 @@ import sys
 from collections import defaultdict
 
 
+def kernel_key(name):
+    if "k_closure_join" in name:
+        return "k_closure_join"
+    if "k_bundles<1," in name:
+        return "k_bundles<1>"
+    if "k_bundles<16," in name:
+        return "k_bundles<16>"
+    if "k_publish" in name:
+        return "k_publish"
+    if "k_gather<" in name:
+        return "k_gather<" + name.split("k_gather<")[1].split(">")[0] + ">"
+    return None
+
+
 def per_kernel(path, counter):
     tot, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(path, recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter or "k_bundles" not in r["Kernel_Name"]:
+            if r["Counter_Name"] != counter:
                 continue
-            k = "k_bundles<1>" if "k_bundles<1," in r["Kernel_Name"] else "k_bundles<16>"
+            k = kernel_key(r["Kernel_Name"])
+            if k is None:
+                continue
             tot[k] += float(r["Counter_Value"])
             launches[k].add(r["Dispatch_Id"])
-    return {k: tot[k] / len(launches[k]) * 1024 for k in tot}  # bytes per launch
+    return {k: tot[k] / len(launches[k]) * 1024 for k in tot}, {k: len(v) for k, v in launches.items()}
+
+
+def kernel_stats(out):
+    rows = {}
+    for f in glob.glob(f"{out}/kt/**/*kernel_stats.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = kernel_key(r["Name"])
+            if k:
+                rows[k] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                           "total_ms": float(r["TotalDurationNs"]) / 1e6}
+    return rows
 
 
 def main(out):
-    fetch = per_kernel(f"{out}/fetch/**/*counter_collection.csv", "FETCH_SIZE")
-    write = per_kernel(f"{out}/write/**/*counter_collection.csv", "WRITE_SIZE")
-    res = {"fetch_bytes_raw": fetch, "write_bytes": write}
-    res["hbm_bytes_per_batch"] = int(sum(2 * v for v in fetch.values()) + sum(write.values()))
-    res["correction"] = "FETCH_SIZE x2 (gfx950) + WRITE_SIZE; both kernels of one batch"
+    gf, _ = per_kernel(f"{out}/gfetch/**/*counter_collection.csv", "FETCH_SIZE")
+    gw, _ = per_kernel(f"{out}/gwrite/**/*counter_collection.csv", "WRITE_SIZE")
+    lanes = 1 << 24
+    calib = {}
+    for k, v in gf.items():
+        width = int(k[len("k_gather<"):-1])
+        calib[width] = {"fetch_reported": v, "read_bytes": lanes * width, "factor": lanes * width / v if v else None,
+                        "write_reported": gw.get(k), "write_bytes": lanes * 4}
+    fetch, n_fetch = per_kernel(f"{out}/fetch/**/*counter_collection.csv", "FETCH_SIZE")
+    write, n_write = per_kernel(f"{out}/write/**/*counter_collection.csv", "WRITE_SIZE")
+    stage_a = [k for k in ("k_closure_join", "k_bundles<1>") if k in fetch]
+    f32 = (calib.get(32) or {}).get("factor") or 2.0
+    f64 = (calib.get(64) or {}).get("factor") or 2.0
+    factor = (f32 + f64) / 2
+    raw = sum(fetch[k] for k in stage_a)
+    res = {
+        "calibration": calib,
+        "fetch_bytes_raw_per_launch": fetch, "write_bytes_per_launch": write, "launches": n_fetch,
+        "fetch_factor_used": factor,
+        "hbm_bytes_per_batch": int(raw * factor + sum(write.get(k, 0) for k in stage_a)),
+        "hbm_bytes_per_batch_raw": int(raw + sum(write.get(k, 0) for k in stage_a)),
+        "kernels": stage_a,
+        "kernel_stats": kernel_stats(out),
+        "correction": "FETCH_SIZE x the gather_probe factor (mean of the 32-B and 64-B random-read factors) "
+                      "+ WRITE_SIZE, summed over the stage-A kernels of one batch",
+    }
     print(json.dumps(res, indent=1))
 
 
