@@ -118,6 +118,9 @@ struct Workspace {
   uint8_t* b_xperm = nullptr; // host batch: where the results' D2H lands — the pinned staging, or
   int32_t* b_xerr = nullptr;  // the caller's buffers themselves when they are gck_host_alloc memory
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
+  bool b_closure = false;     // stage A began with the closure join: its leftovers are bundled in finish
+  bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
+  uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
   unsigned b_seq = 0;         // publish sequence of stage A
   float b_ms = 0.f;
   // ---- grid-wide path (allocated on first use: ensure_wide) --------------------------------
@@ -1782,6 +1785,21 @@ static bool program_in_lds(const Ctx& c) {
   return prog_bytes <= (size_t)kProgBytes;
 }
 
+static void launch_wave_bundles(Engine& e, Workspace& w, const Ctx& c, const BundleArgs& a, hipStream_t st) {
+  const bool prog_lds = program_in_lds(c);
+  // bidirectional instantiation only when the snapshot has an eligible permission (bidir.inc)
+  const bool bd = e.dev->has_bidir;
+  if (prog_lds && bd)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else if (prog_lds)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else if (bd)
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  else
+    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
+  HIP_OK(hipGetLastError());
+}
+
 // Stage A of a bundle batch (n <= max_batch): the persistent wave-bundle kernel over every
 // check, then — for a host batch — the copy of the results into the pinned staging, and the
 // publication the host spins on. Nothing waits here.
@@ -1794,13 +1812,16 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   if (timing_env) HIP_OK(hipMemsetAsync(w.timing, 0, w.timing_cap * 8, st));
   if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));  // + b_ctrs
   w.ctr_clean = false;
-  // one event opens the batch and stage A, one closes stage A: every record is a host API call
-  // on the per-batch path
-  HIP_OK(hipEventRecord(w.ev0, st));
-  // the closure-join stage answers the nested-group checks it can (closure.inc); the bundle
-  // kernel then takes what it left, reading the count on the device
+  // GCK_FLAG_PROFILE: one event opens stage A, one closes it, on every 4th batch of the workspace
+  // (each record is a host API call on the per-batch path)
+  w.b_timed = (e.cfg.flags & GCK_FLAG_PROFILE) && (w.n_batches++ % 4 == 0);
+  if (w.b_timed) HIP_OK(hipEventRecord(w.ev0, st));
+  // the closure-join stage answers the nested-group checks it can (closure.inc); what it leaves is
+  // counted in the published counters and bundled by bundles_finish, so the common batch is two
+  // launches: the join and the publication
   const DeviceSnapshot& ds = *e.dev;
-  if (ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE)) {
+  w.b_closure = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
+  if (w.b_closure) {
     CjArgs j{};
     j.items = d_items;
     j.n = n;
@@ -1817,22 +1838,10 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_entries = ds.cj_o_entries;
     hipLaunchKernelGGL(k_closure_join, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
     HIP_OK(hipGetLastError());
-    a.idx = w.c_deferred;
-    a.n_dev = w.b_ctrs + 4;
+  } else {
+    launch_wave_bundles(e, w, c, a, st);
   }
-  const bool prog_lds = program_in_lds(c);
-  // bidirectional instantiation only when the snapshot has an eligible permission (bidir.inc)
-  const bool bd = e.dev->has_bidir;
-  if (prog_lds && bd)
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
-  else if (prog_lds)
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, true, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
-  else if (bd)
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, true>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
-  else
-    hipLaunchKernelGGL((k_bundles<1, kLFWave, false, false>), dim3(w.b_blocks), dim3(bundle_block<1>()), 0, st, c, a);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(w.ev1, st));
+  if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
   if (host_out) {
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
@@ -1850,10 +1859,41 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   wait_published(w, st, w.b_seq);
   add_counters(e, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
-  const bool profile = (e.cfg.flags & GCK_FLAG_PROFILE) != 0;
+  const bool profile = w.b_timed;
   float ms = 0.f, bm = 0.f, gm = 0.f;
-  elapsed_ms(&ms, w.ev0, w.ev1);
+  if (w.b_timed) elapsed_ms(&ms, w.ev0, w.ev1);
   bm = ms;
+  const uint32_t n_cj = w.b_closure ? w.h_bctrs[4] : 0u;
+  if (n_cj > n) throw Error(GCK_E_DEVICE, "engine invariant violated: closure-join deferred count");
+  if (n_cj > 0) {
+    // the checks the closure join left: the wave bundles over its list (the publish zeroed the
+    // count on the device: restore it first)
+    Ctx c = make_ctx(e, w, now_us);
+    c.ck_items = d_items;
+    BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
+    a.idx = w.c_deferred;
+    a.n_dev = w.b_ctrs + 4;
+    w.h_seq[2] = n_cj;
+    HIP_OK(hipMemcpyAsync(w.b_ctrs + 4, w.h_seq + 2, sizeof(unsigned), hipMemcpyHostToDevice, st));
+    w.ctr_clean = false;
+    if (w.b_timed) HIP_OK(hipEventRecord(w.ev0, st));
+    launch_wave_bundles(e, w, c, a, st);
+    if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
+    if (host_out) {
+      HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    }
+    publish_launch(w, st);
+    wait_published(w, st, w.b_seq);
+    add_counters(e, *w.h_ctr);
+    w.ctr_clean = true;
+    if (w.b_timed) {
+      float am = 0.f;
+      elapsed_ms(&am, w.ev0, w.ev1);
+      ms += am;
+      bm += am;
+    }
+  }
   const uint32_t n_def = w.h_bctrs[1];
   uint32_t n_def2 = n_def;
   const bool giant = !(e.cfg.flags & GCK_FLAG_NO_GIANT);
@@ -1882,7 +1922,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     w.h_seq[1] = n_def;
     HIP_OK(hipMemcpyAsync(w.b_ctrs + 1, w.h_seq + 1, sizeof(unsigned), hipMemcpyHostToDevice, st));
     w.ctr_clean = false;
-    HIP_OK(hipEventRecord(w.ev0, st));
+    if (w.b_timed) HIP_OK(hipEventRecord(w.ev0, st));
     if (program_in_lds(c))
       hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, true, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
@@ -1890,12 +1930,12 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
       hipLaunchKernelGGL((k_bundles<kGiantWaves, kLFGiant, false, false>), dim3(w.g_slots),
                          dim3(bundle_block<kGiantWaves>()), 0, st, c, g);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(w.ev1, st));
+    if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
     publish_launch(w, st);
     wait_published(w, st, w.b_seq);
     add_counters(e, *w.h_ctr);
     w.ctr_clean = true;
-    elapsed_ms(&gm, w.ev0, w.ev1);
+    if (w.b_timed) elapsed_ms(&gm, w.ev0, w.ev1);
     ms += gm;
     n_def2 = w.h_bctrs[3];
     if (n_def2 > n_def) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred count");

@@ -186,14 +186,16 @@ typedef struct gck_stats {
   uint64_t queries;            /* queries allocated (checks + join operands) */
   uint64_t joins;              /* intersection/exclusion/all() joins spawned */
   uint64_t retries;            /* batch splits after a workspace overflow */
-  double kernel_ms;            /* device time of the last gck_check_bulk* call (HIP events) */
+  double kernel_ms;            /* GCK_FLAG_PROFILE: device time of the last call's batches that were
+                                  timed (HIP events around stage A on every 4th batch of a workspace) */
   double expand_ms;            /* GCK_FLAG_PROFILE: summed k_expand time (all batches) */
   double edges_ms;             /* GCK_FLAG_PROFILE: summed k_edges time */
   double resolve_ms;           /* GCK_FLAG_PROFILE: summed k_resolve time */
   uint64_t expand_launches;    /* GCK_FLAG_PROFILE: k_expand launches timed */
   uint64_t edges_launches;     /* GCK_FLAG_PROFILE: k_edges launches timed */
-  double bundle_ms;            /* GCK_FLAG_PROFILE: summed wavefront-bundle kernel time */
-  uint64_t bundle_launches;    /* GCK_FLAG_PROFILE: bundle launches timed */
+  double bundle_ms;            /* GCK_FLAG_PROFILE: summed stage-A time (closure join and/or wave
+                                  bundles) of the timed batches (every 4th of a workspace) */
+  uint64_t bundle_launches;    /* GCK_FLAG_PROFILE: batches whose stage A was timed */
   uint64_t deferred;           /* checks handed from wavefront bundles to workgroup bundles */
   double giant_ms;             /* GCK_FLAG_PROFILE: summed workgroup-bundle kernel time */
   uint64_t deferred_wide;      /* checks handed from workgroup bundles to the grid-wide path */

@@ -21,3 +21,8 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output
 echo "pmc done"
 python3 tools/traffic_summary.py "$OUT" > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
+# keep the summaries (kernel stats, counter totals via traffic.json); drop the per-dispatch traces so
+# that gpurun_out stays under the 64 MiB copy-back limit
+find "$OUT" -name "*kernel_trace.csv" -delete
+find "$OUT" -name "*counter_collection.csv" -delete
+find "$OUT" -name "*agent_info.csv" -delete

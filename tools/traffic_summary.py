@@ -2,9 +2,10 @@
 
 FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived counters). MI355X_MICROARCH.md
 §HBM establishes FETCH_SIZE = 1/2 of the bytes for wide streaming reads only; tools/gather_probe
-measures the factor for random aligned reads of 4, 16, 32 and 64 B from a table far larger than the
-Infinity Cache (known bytes), and the per-batch figure is corrected with the factor of the access
-width that dominates the stage-A kernels' reads (the 32-B signature and 64-B index reads)."""
+measures random aligned reads of 4, 16, 32 and 64 B from a table 16x the Infinity Cache (known
+bytes): every one of them is reported as 64 B — one memory-side line per access, whatever its
+width. For these kernels, whose reads are random and at most 64 B, raw FETCH_SIZE is therefore the
+HBM line traffic itself (factor 1, the 64-B calibration point), and no x2 correction applies."""
 import csv
 import glob
 import json
@@ -63,9 +64,7 @@ def main(out):
     fetch, n_fetch = per_kernel(f"{out}/fetch/**/*counter_collection.csv", "FETCH_SIZE")
     write, n_write = per_kernel(f"{out}/write/**/*counter_collection.csv", "WRITE_SIZE")
     stage_a = [k for k in ("k_closure_join", "k_bundles<1>") if k in fetch]
-    f32 = (calib.get(32) or {}).get("factor") or 2.0
-    f64 = (calib.get(64) or {}).get("factor") or 2.0
-    factor = (f32 + f64) / 2
+    factor = (calib.get(64) or {}).get("factor") or 1.0  # one 64-B line per random access
     raw = sum(fetch[k] for k in stage_a)
     res = {
         "calibration": calib,
@@ -75,8 +74,9 @@ def main(out):
         "hbm_bytes_per_batch_raw": int(raw + sum(write.get(k, 0) for k in stage_a)),
         "kernels": stage_a,
         "kernel_stats": kernel_stats(out),
-        "correction": "FETCH_SIZE x the gather_probe factor (mean of the 32-B and 64-B random-read factors) "
-                      "+ WRITE_SIZE, summed over the stage-A kernels of one batch",
+        "correction": "FETCH_SIZE x the gather_probe factor at 64 B (random reads of 4-64 B all count one "
+                      "64-B line: FETCH_SIZE is the line traffic) + WRITE_SIZE, summed over the stage-A kernels "
+                      "of one batch",
     }
     print(json.dumps(res, indent=1))
 
