@@ -467,14 +467,17 @@ def main():
         line = {
             "metric": ("permission checks/sec (whole node) at batch 64K, 1B tuples" if WL.kind == "nested" else
                        f"permission checks/sec (whole node) at batch 64K, {WL.cfg['workload']}"),
-            "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 1), "unit": "checks/s", "n_gpus": 1 if args.share_gpu else world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": WL.data,
             "config": {**WL.cfg, "tuples": n_tuples, "batch_per_gpu": args.batch,
                        "parallelism": (f"graph partitioned x{world} by resource id, per-level all-to-all "
                                        f"({args.part_backend}), global batch {args.batch * world}")
-                       if args.partitioned else f"batch-sharded x{world}, graph replicated",
+                       if args.partitioned else
+                       (f"batch-sharded x{world} (rank r checks the r-th contiguous slice of a {args.batch * world}"
+                        f"-check request, gochugaru_amd/sharded.py), graph replicated, no data-path collective"
+                        + (f", {world} ranks sharing one GPU" if args.share_gpu else "")),
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
             "roofline": roof, "cpu_baseline": cpu,
             **({"host_buffers": host_rate} if host_rate else {}),
