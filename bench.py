@@ -66,10 +66,11 @@ def parse():
                          "global batch (batch x ranks) with a per-level all-to-all (gochugaru_amd/partition.py)")
     ap.add_argument("--part-backend", default="nccl", help="exchange backend in --partitioned mode (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank on cuda:0 (a one-GPU rehearsal with gloo)")
-    ap.add_argument("--config", default="nested", choices=["nested", "gdocs", "github", "mixed"],
+    ap.add_argument("--config", default="nested", choices=["nested", "gdocs", "github", "mixed", "quota"],
                     help="nested = BASELINE config 4 (the headline, default); gdocs / github = configs 2 / 3 "
                          "(tests/synth_configs.py) at --scale; mixed = config 5 (config 2 + 10 %% caveated "
-                         "tuples, check contexts, one Watch batch of --churn x tuples applied per step)")
+                         "tuples, check contexts, one Watch batch of --churn x tuples applied per step); quota = "
+                         "config 5 with 32K per-relationship caveat contexts x one context per request")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     return ap.parse_args()
@@ -107,6 +108,23 @@ class Workload:
                                            (H["viewer_off"], H["viewer_nbr"], None, None, G.n_docs)])
                 return corc.encode_program(ids, idx), tab
             self.oracle = oracle
+        elif args.config == "quota":
+            from tests import synth_configs
+            Q = self.Q = synth_configs.Quota(args.scale, device=dev)
+            W = Q.W
+            self.schema = W.schema
+            self.reserve = [(W.t(t), n) for t, n in W.counts.items()]
+            self.csrs = None
+            self.union_only = True
+            self.data = (f"synthetic (tests/synth_configs.py Quota, seed 20251003, scale {args.scale}): config-2 graph, "
+                         f"10% of folder/doc viewer+editor user tuples caveated with quota(limit, used) "
+                         f"{{used < limit}}, each relationship storing one of {len(Q.limits)} distinct limits "
+                         f"(as many partial caveat instances); every check carries its own {{\"used\": U}} "
+                         f"context (10% none): {args.batch} contexts per batch")
+            self.cfg = {"workload": W.name, **{k + "s": v for k, v in W.counts.items()},
+                        "caveat_instances": len(Q.limits), "contexts_per_batch": args.batch}
+            self._checks = lambda n, seed: Q.checks(n, seed)
+            self.oracle = None
         elif args.config == "mixed":
             from tests import synth_configs
             M = self.M = synth_configs.Mixed(args.scale, device=dev)
@@ -151,7 +169,9 @@ class Workload:
             nbr32 = nbr.contiguous()
             keep.append((off32, nbr32))
             eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr32.data_ptr(), nbr32.numel(), device=True)
-        if self.kind == "mixed":
+        if self.kind == "quota":
+            self.Q.load(eng, loader)
+        elif self.kind == "mixed":
             self.cav = eng.add_caveat_instance("only_on_tuesday", "")
             self.M.load(eng, loader, self.cav)
         else:
@@ -231,6 +251,24 @@ def main():
             rev["apply_s"] += time.perf_counter() - t_a
             eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream,
                                   contexts=CONTEXTS)
+    elif WL.kind == "quota":
+        # per step one batch with its own 64K contexts (pre-generated, rotated): the contexts are
+        # parsed, the walk records the (instance, context) pairs it meets, the host evaluates
+        # them and the batch runs again — all inside the step
+        from gochugaru_amd.engine import Contexts  # marshalled ahead, as the items are
+        q_rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(args.warmup + args.steps)]
+        q_rot = [(it, used, Contexts(texts)) for it, used, texts in q_rot]
+        q_out = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
+                  torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in q_rot]
+        torch.cuda.synchronize()
+        cursor = {"k": 0}
+
+        def step():
+            k = cursor["k"]
+            cursor["k"] += 1
+            it, _, texts = q_rot[k]
+            eng.check_bulk_device(it.data_ptr(), args.batch, q_out[k][0].data_ptr(), q_out[k][1].data_ptr(),
+                                  stream=stream, contexts=texts)
     else:
         # distinct batches, rotated through warm-up and timed steps (no step re-reads a batch a
         # previous step left in the caches), each with its own result buffers; up to `depth`
@@ -258,7 +296,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if WL.kind != "mixed" and not args.partitioned:
+    if WL.kind not in ("mixed", "quota") and not args.partitioned:
         drain()
     torch.cuda.synchronize()
     eng.reset_stats()
@@ -268,14 +306,16 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if WL.kind != "mixed" and not args.partitioned:
+    if WL.kind not in ("mixed", "quota") and not args.partitioned:
         drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if WL.kind != "mixed" and not args.partitioned:  # the first timed batch and its results
+    if WL.kind not in ("mixed", "quota") and not args.partitioned:  # the first timed batch and its results
         items, (perm, err) = rot[args.warmup], outs[args.warmup]
+    if WL.kind == "quota":
+        items, (perm, err) = q_rot[args.warmup][0], q_out[args.warmup]
     st = eng.stats()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -297,7 +337,7 @@ def main():
     # the same rotated batches, `depth` in flight (gck_check_submit with host buffers: each
     # batch's copies overlap the other batches' kernels), and one at a time for reference.
     host_rate = None
-    if WL.kind != "mixed" and not args.partitioned and args.host_steps > 0:
+    if WL.kind not in ("mixed", "quota") and not args.partitioned and args.host_steps > 0:
         h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot]
         ref0 = (outs[args.warmup][0].cpu().numpy(), outs[args.warmup][1].cpu().numpy())
         # the same batches in pinned host memory (gck_host_alloc: DMA straight from / into them)
@@ -345,7 +385,21 @@ def main():
         hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
         cp, ce = WL.M.expected(hi, threads=args.cpu_threads or min(16, os.cpu_count() or 1))
         agree_mixed = float(((cp == res) & (ce == errs)).mean())
-    if rank == 0 and not args.no_oracle and WL.kind != "mixed":
+    if rank == 0 and not args.no_oracle and WL.kind == "quota":
+        from oracle import corc  # the first timed batch vs the C oracle's threshold mode
+        q_threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        q_prog, q_tab, q_lim = WL.Q.oracle()
+        hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+        t_q = time.perf_counter()
+        cp, ce = corc.check_quota(q_prog, q_tab, hi, q_lim, q_rot[args.warmup][1], threads=q_threads)
+        t_q = time.perf_counter() - t_q
+        agree_mixed = float(((cp == res) & (ce == errs)).mean())
+        if not args.no_cpu and world == 1:
+            cpu_q = {"value": round(args.batch / t_q, 1), "unit": "checks/s", "cores": q_threads, "kind": "port",
+                     "sample": f"the first timed batch ({args.batch} checks, {args.batch} contexts), C oracle "
+                               f"threshold mode (oracle/check_oracle.c orc_check_quota: the caveat restated in C, "
+                               f"no CEL), OpenMP {q_threads} threads, {t_q:.2f}s"}
+    if rank == 0 and not args.no_oracle and WL.kind not in ("mixed", "quota"):
         from oracle import corc
 
         prog, tab = WL.oracle()
@@ -456,8 +510,10 @@ def main():
                          f"= the box's CPU share; nproc reports {os.cpu_count()}), {dt:.1f}s; every sampled check "
                          f"compared with the GPU result"}
 
-    if rank == 0 and WL.kind == "mixed" and not args.no_oracle:
+    if rank == 0 and WL.kind in ("mixed", "quota") and not args.no_oracle:
         agree = agree_mixed
+    if rank == 0 and WL.kind == "quota" and not args.no_oracle and not args.no_cpu and world == 1:
+        cpu = cpu_q
 
     if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
         cp, ce, _ = corc.check(prog, tab, host_items, threads=threads)
@@ -496,6 +552,9 @@ def main():
                        "giant_ms_per_batch": round(st["giant_ms"] / n_batches, 4),
                        "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
+            **({"caveats": {"evals_per_step": round(st["caveat_evals"] / args.steps, 1),
+                            "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}
+               if WL.kind == "quota" else {}),
             **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warmup + args.steps) * 1e3, 3),
                           "revision": rev["r"]}} if WL.kind == "mixed" else {}),
         }

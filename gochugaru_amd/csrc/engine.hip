@@ -27,7 +27,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
 #include <type_traits>
 
 #include "engine.hpp"
@@ -169,10 +171,27 @@ struct Workspace {
   gck_item* def_items = nullptr;
   uint8_t* def_perm = nullptr;
   int32_t* def_err = nullptr;
-  // the current call's caveat outcome table (gck_api.cpp caveat_table), n_ctx columns
+  // the current call's check-time caveat contexts (engine.hpp CavCall): its dense outcome table,
+  // or the lazy evaluation's device map of the pairs evaluated so far (cav_keys / cav_vals, open
+  // addressing, host-built) and the set / list of the unevaluated pairs a pass touched
+  CavCall cav;
+  bool cav_on = false;          // the call has contexts and the snapshot partial instances
+  bool cav_lazy = false;
   uint8_t* cav_dyn = nullptr;
   size_t cav_dyn_cap = 0;
-  uint32_t n_ctx = 0;
+  uint32_t* cav_slot = nullptr;  // dense: each slot's distinct context (CavCall::of_slot)
+  size_t cav_slot_cap = 0;
+  unsigned long long* cav_keys = nullptr;
+  uint8_t* cav_vals = nullptr;
+  size_t cav_map_cap = 0;       // slots of the device map (a power of two)
+  size_t cav_map_alloc = 0;
+  std::unordered_map<unsigned long long, uint8_t> cav_eval;  // host: the pairs evaluated for the call
+  std::unordered_map<uint32_t, cel::Object> cav_parsed;       // host: the call's contexts parsed so far
+  unsigned long long* req_set = nullptr;  // kReqSet slots
+  unsigned long long* req_list = nullptr; // kReqCap pairs
+  unsigned* req_cnt = nullptr;
+  uint8_t* cav_flag = nullptr;  // per check of the batch: its walk touched a pair whose evaluation failed
+  uint32_t b_cav_req = 0, b_cav_err = 0;  // the published cav_requests / cav_errors of the batch's pass
   // lookups (lookup.inc): matching ids / permissionships of one candidate chunk, their count
   uint32_t* lk_ids = nullptr;
   uint8_t* lk_perm = nullptr;
@@ -211,14 +230,26 @@ struct Ctx {
   uint32_t level, max_depth;
   const unsigned long long* hgt;  // per forward node: its heights array (u32 per object) or 0
   int64_t now_us;
-  // caveats (cel.hpp; gck_api.cpp caveat_table): per instance its outcome under the stored
+  // caveats (cel.hpp; gck_api.cpp caveat_call): per instance its outcome under the stored
   // context alone (0 false, 1 true, 2 partial) and, for partial ones, a row of the per-batch
   // table of outcomes under each check context (column slot - 1)
   const uint8_t* cav_static;
   const uint32_t* cav_row;
   const uint8_t* cav_dyn;
+  const uint32_t* cav_slot;
   const gck_item* ck_items;  // the launch's items: check k's context slot
-  uint32_t n_ctx;
+  uint32_t n_ctx, n_dist;
+  // lazy evaluation (cav_keys non-null): the evaluated pairs, and where a pass records the rest
+  const unsigned long long* cav_keys;
+  const uint8_t* cav_vals;
+  uint64_t cav_kmask;
+  unsigned long long* req_set;
+  unsigned long long* req_list;
+  unsigned* req_cnt;
+  // check k of the launch is check ck_map[k] (or ck_off + k) of the batch: its cav_flag byte
+  uint8_t* cav_flag;
+  const uint32_t* ck_map;
+  uint32_t ck_off;
   // partitioned graphs (partition.inc): entries for objects another rank owns go to its outbox
   // region [d * out_cap, (d + 1) * out_cap) instead of the next frontier
   uint32_t rank, world;
@@ -227,7 +258,7 @@ struct Ctx {
   uint32_t out_cap;
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
   x ^= x >> 33;
@@ -390,18 +421,61 @@ __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t n
   return x == 0 || x > now_us;
 }
 
+// Lazy caveat evaluation: the outcome of (partial instance row, context slot) from the map of
+// pairs the host has evaluated, else 4 after recording the pair for the host (once per pass; a
+// pass that overruns kReqCap leaves the rest to the next).
+constexpr uint32_t kReqCap = 1u << 18;
+constexpr uint32_t kReqSet = 1u << 20;
+
+__device__ __noinline__ uint32_t cav_lazy(const Ctx& c, uint32_t row, uint32_t slot) {
+  const unsigned long long key = ((unsigned long long)row << 32) | slot;
+  uint64_t h = mix64(key) & c.cav_kmask;
+  for (int p = 0; p < 64; ++p) {  // the host keeps the map at most half full
+    const unsigned long long k = gptr(c.cav_keys)[h];
+    if (k == key) return gptr(c.cav_vals)[h];
+    if (k == kEmptyKey) break;
+    h = (h + 1) & c.cav_kmask;
+  }
+  atomicAdd(&c.ctr->cav_requests, 1u);
+  if (__hip_atomic_load(c.req_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kReqCap) return 4u;
+  uint64_t s = mix64(key) & (kReqSet - 1);
+  for (int p = 0; p < 128; ++p) {
+    const unsigned long long v = __hip_atomic_load(&c.req_set[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == key) return 4u;
+    if (v == kEmptyKey) {
+      const unsigned long long prev = atomicCAS(&c.req_set[s], kEmptyKey, key);
+      if (prev == kEmptyKey) {
+        const unsigned idx = atomicAdd(c.req_cnt, 1u);
+        if (idx < kReqCap) gptr_w(c.req_list)[idx] = key;
+        return 4u;
+      }
+      if (prev == key) return 4u;
+    }
+    s = (s + 1) & (kReqSet - 1);
+  }
+  return 4u;
+}
+
 // Caveat instance `cav` on a path of the check whose item is `item`: 0 = the caveat is false
-// (the relationship does not count), 1 = true (a plain edge), 2 = unresolved (CONDITIONAL).
+// (the relationship does not count), 1 = true (a plain edge), 2 = unresolved (CONDITIONAL). A
+// pair whose evaluation failed marks the check (it ends with GCK_ITEM_ERR_CAVEAT_EVAL) and a
+// pair not evaluated yet reads as unresolved (the batch runs again once it is).
 __device__ __forceinline__ uint32_t cav_state(const Ctx& c, uint32_t cav, uint32_t item) {
   const uint32_t s = gptr(c.cav_static)[cav];
   if (s != 2u || c.n_ctx == 0) return s;
   const uint32_t slot = gptr(c.ck_items)[item].context_slot;
   if (slot == 0 || slot > c.n_ctx) return 2u;
-  return gptr(c.cav_dyn)[(size_t)gptr(c.cav_row)[cav] * c.n_ctx + (slot - 1)];
+  const uint32_t row = gptr(c.cav_row)[cav];
+  const uint32_t v = c.cav_keys ? cav_lazy(c, row, slot)
+                                : (uint32_t)gptr(c.cav_dyn)[(size_t)row * c.n_dist + gptr(c.cav_slot)[slot - 1]];
+  if (v == 3u) {
+    const uint32_t k = c.ck_map ? gptr(c.ck_map)[item] : c.ck_off + item;
+    gptr_w(c.cav_flag)[k] = 1;
+    atomicAdd(&c.ctr->cav_errors, 1u);
+  }
+  return v > 2u ? 2u : v;
 }
 
-// An edge of an ext CSR under the check of `item`: 0 = absent (expired, or its caveat is
-// false), 1 = plain, 2 = conditional.
 __device__ __forceinline__ uint32_t ext_state(const Ctx& c, const DevCSR& r, uint32_t pos, uint32_t item) {
   if (!visible(r, pos, c.now_us)) return 0u;
   return cav_state(c, csr_cav(r, pos), item);
@@ -1590,11 +1664,24 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.cav_static = ds.cav_static;
   c.cav_row = ds.cav_row;
   c.cav_dyn = w.cav_dyn;
-  c.n_ctx = w.cav_dyn ? w.n_ctx : 0u;
+  c.cav_slot = w.cav_slot;
+  c.n_ctx = w.cav_on ? w.cav.n_ctx : 0u;
+  c.n_dist = w.cav.n_dist;
+  c.cav_keys = w.cav_lazy ? w.cav_keys : nullptr;
+  c.cav_vals = w.cav_vals;
+  c.cav_kmask = w.cav_map_cap ? w.cav_map_cap - 1 : 0;
+  c.req_set = w.req_set;
+  c.req_list = w.req_list;
+  c.req_cnt = w.req_cnt;
+  c.cav_flag = w.cav_flag;
+  c.ck_map = nullptr;
+  c.ck_off = 0;
   return c;
 }
 
-static void add_counters(Engine& e, const DevCounters& h) {
+static void add_counters(Engine& e, Workspace& w, const DevCounters& h) {
+  w.b_cav_req += h.cav_requests;
+  w.b_cav_err += h.cav_errors;
   std::lock_guard<std::mutex> lk(e.stats_mu);
   e.stats.entries_expanded += h.expanded;
   e.stats.row_lookups += h.row_lookups;
@@ -1608,12 +1695,15 @@ static void add_counters(Engine& e, const DevCounters& h) {
 }
 
 // Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
-// (the caller splits the batch).
+// (the caller splits the batch). Its check k is check map[k] (map null: pos + k) of the batch.
 static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
-                      uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out) {
+                      uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out, size_t pos,
+                      const uint32_t* map) {
   ensure_wide(w);
   Ctx c = make_ctx(e, w, now_us);
   c.ck_items = d_items;
+  c.ck_map = map;
+  c.ck_off = map ? 0u : (uint32_t)pos;
   HIP_OK(hipEventRecord(w.ev0, st));
   w.ctr_clean = false;
   HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));
@@ -1674,7 +1764,7 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   HIP_OK(hipEventElapsedTime(&ms, w.ev0, w.ev1));
   *ms_out += ms;
   const DevCounters& h = *w.h_ctr;
-  add_counters(e, h);
+  add_counters(e, w, h);
   std::lock_guard<std::mutex> lk(e.stats_mu);
   e.stats.levels += levels;
   e.stats.queries += h.n_queries;
@@ -1683,12 +1773,15 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
   return true;
 }
 
+// map: the batch index of each of the n checks (null: they are the batch)
 static void check_range_wide(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us,
-                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms) {
+                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms,
+                             const uint32_t* map = nullptr) {
   size_t pos = 0;
   while (pos < n) {
     size_t len = std::min(n - pos, w.max_batch);
-    while (!run_batch(e, w, d_items + pos, (uint32_t)len, now_us, d_perm + pos, d_err + pos, st, ms)) {
+    while (!run_batch(e, w, d_items + pos, (uint32_t)len, now_us, d_perm + pos, d_err + pos, st, ms, pos,
+                      map ? map + pos : nullptr)) {
       {
         std::lock_guard<std::mutex> lk(e.stats_mu);
         e.stats.retries++;
@@ -1857,7 +1950,7 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n);
 static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   wait_published(w, st, w.b_seq);
-  add_counters(e, *w.h_ctr);
+  add_counters(e, w, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
   const bool profile = w.b_timed;
   float ms = 0.f, bm = 0.f, gm = 0.f;
@@ -1885,7 +1978,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     }
     publish_launch(w, st);
     wait_published(w, st, w.b_seq);
-    add_counters(e, *w.h_ctr);
+    add_counters(e, w, *w.h_ctr);
     w.ctr_clean = true;
     if (w.b_timed) {
       float am = 0.f;
@@ -1933,7 +2026,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
     publish_launch(w, st);
     wait_published(w, st, w.b_seq);
-    add_counters(e, *w.h_ctr);
+    add_counters(e, w, *w.h_ctr);
     w.ctr_clean = true;
     if (w.b_timed) elapsed_ms(&gm, w.ev0, w.ev1);
     ms += gm;
@@ -1961,7 +2054,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     const uint32_t grid = (n_def2 + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, d_items, def_idx, n_def2, w.def_items);
     HIP_OK(hipGetLastError());
-    check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, &ms);
+    check_range_wide(e, w, w.def_items, n_def2, now_us, w.def_perm, w.def_err, st, &ms, def_idx);
     hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(kBlock), 0, st, def_idx, n_def2, w.def_perm, w.def_err, d_perm,
                        d_err);
     HIP_OK(hipGetLastError());
@@ -2015,24 +2108,151 @@ static int64_t wall_now_us() {
   return duration_cast<microseconds>(system_clock::now().time_since_epoch()).count();
 }
 
-// Stages the call's caveat outcome table (n_ctx columns; empty = no check contexts).
-static void stage_caveats(Workspace& w, const std::vector<uint8_t>& table, uint32_t n_ctx, hipStream_t st) {
-  w.n_ctx = table.empty() ? 0u : n_ctx;
-  if (table.empty()) return;
-  if (w.cav_dyn_cap < table.size()) {
-    if (w.cav_dyn) {
-      HIP_OK(hipStreamSynchronize(st));
-      w.allocs.erase(std::remove(w.allocs.begin(), w.allocs.end(), (void*)w.cav_dyn), w.allocs.end());
-      HIP_OK(hipFreeAsync(w.cav_dyn, nullptr));
-      w.cav_dyn = nullptr;
-    }
-    w.cav_dyn_cap = std::max(table.size(), w.cav_dyn_cap * 2);
-    w.cav_dyn = dalloc<uint8_t>(w.allocs, w.cav_dyn_cap);
-    HIP_OK(hipStreamSynchronize(nullptr));  // the allocation is ordered on the null stream
+// ---- check-time caveat contexts (engine.hpp CavCall) -----------------------------------------
+
+__global__ void k_cav_fail(const uint8_t* flag, uint32_t n, uint8_t* perm, int32_t* err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) {
+    perm[i] = GCK_PERM_UNSPECIFIED;
+    err[i] = GCK_ITEM_ERR_CAVEAT_EVAL;
   }
-  // pageable source: the copy has completed when the call returns, so the table may go
-  HIP_OK(hipMemcpyAsync(w.cav_dyn, table.data(), table.size(), hipMemcpyHostToDevice, st));
+}
+
+template <class T>
+static void grow(Workspace& w, T*& p, size_t& cap, size_t want) {
+  if (cap >= want) return;
+  if (p) {
+    HIP_OK(hipDeviceSynchronize());
+    w.allocs.erase(std::remove(w.allocs.begin(), w.allocs.end(), (void*)p), w.allocs.end());
+    HIP_OK(hipFree(p));
+    p = nullptr;
+  }
+  cap = std::max(want, cap * 2);
+  HIP_OK(hipMalloc(&p, cap * sizeof(T)));
+  w.allocs.push_back(p);
+}
+
+// Uploads the lazy map: every pair evaluated so far, open addressing at most half full.
+static void upload_cav_map(Workspace& w, hipStream_t st) {
+  size_t cap = 1024;
+  while (cap < 2 * w.cav_eval.size()) cap *= 2;
+  if (w.cav_map_alloc < cap) {
+    size_t kc = w.cav_map_alloc, vc = w.cav_map_alloc;
+    grow(w, w.cav_keys, kc, cap);
+    grow(w, w.cav_vals, vc, cap);
+    w.cav_map_alloc = std::min(kc, vc);
+  }
+  w.cav_map_cap = cap;
+  std::vector<unsigned long long> keys(cap, kEmptyKey);
+  std::vector<uint8_t> vals(cap, 0);
+  for (const auto& kv : w.cav_eval) {
+    uint64_t h = mix64(kv.first) & (cap - 1);
+    while (keys[h] != kEmptyKey) h = (h + 1) & (cap - 1);
+    keys[h] = kv.first;
+    vals[h] = kv.second;
+  }
+  // pageable sources: complete when the calls return
+  HIP_OK(hipMemcpyAsync(w.cav_keys, keys.data(), cap * 8, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(w.cav_vals, vals.data(), cap, hipMemcpyHostToDevice, st));
   HIP_OK(hipStreamSynchronize(st));
+}
+
+// Stages the call's caveat contexts on the workspace: the dense table, or an empty lazy map
+// and a clear request set.
+static void stage_caveats(Workspace& w, CavCall&& call, hipStream_t st) {
+  w.cav = std::move(call);
+  w.cav_on = w.cav.n_ctx > 0;
+  w.cav_lazy = w.cav_on && w.cav.dense.empty();
+  w.cav_eval.clear();
+  w.cav_parsed.clear();
+  if (!w.cav_on) return;
+  if (!w.cav_flag) {
+    HIP_OK(hipMalloc(&w.cav_flag, std::max<size_t>(w.max_batch, 1)));
+    w.allocs.push_back(w.cav_flag);
+  }
+  if (!w.cav_lazy) {
+    grow(w, w.cav_dyn, w.cav_dyn_cap, w.cav.dense.size());
+    grow(w, w.cav_slot, w.cav_slot_cap, w.cav.of_slot.size());
+    // pageable sources: complete when the calls return
+    HIP_OK(hipMemcpyAsync(w.cav_dyn, w.cav.dense.data(), w.cav.dense.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(w.cav_slot, w.cav.of_slot.data(), w.cav.of_slot.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return;
+  }
+  if (!w.req_set) {
+    w.req_set = dalloc<unsigned long long>(w.allocs, kReqSet);
+    w.req_list = dalloc<unsigned long long>(w.allocs, kReqCap);
+    w.req_cnt = dalloc<unsigned>(w.allocs, 1);
+    HIP_OK(hipStreamSynchronize(nullptr));  // the allocations are ordered on the null stream
+  }
+  HIP_OK(hipMemsetAsync(w.req_set, 0xFF, (size_t)kReqSet * 8, st));
+  HIP_OK(hipMemsetAsync(w.req_cnt, 0, 4, st));
+  upload_cav_map(w, st);
+}
+
+// Evaluates the recorded pairs (row << 32 | slot) on the host, in parallel above a few hundred;
+// an evaluation error is outcome 3.
+// Runs f(lo, hi) over [0, n) on up to 16 host threads (one below `grain` items); the first
+// exception is rethrown.
+template <class F>
+static void host_parallel(size_t n, size_t grain, F&& f) {
+  const size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), (n + grain - 1) / grain});
+  if (nt <= 1) {
+    if (n) f(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  std::vector<std::exception_ptr> ex(nt);
+  for (size_t t = 0; t < nt; ++t)
+    ts.emplace_back([&, t] {
+      try {
+        f(n * t / nt, n * (t + 1) / nt);
+      } catch (...) {
+        ex[t] = std::current_exception();
+      }
+    });
+  for (auto& t : ts) t.join();
+  for (auto& x : ex)
+    if (x) std::rethrow_exception(x);
+}
+
+// Evaluates the recorded pairs (row << 32 | slot) on the host, parsing the contexts they need
+// first (a malformed one fails the call); an evaluation error is outcome 3.
+static void evaluate_pairs(Engine& e, Workspace& w, const std::vector<unsigned long long>& keys) {
+  std::vector<uint32_t> need;
+  for (unsigned long long k : keys) {
+    const uint32_t slot = (uint32_t)k;
+    if (!w.cav_parsed.count(slot)) need.push_back(slot);
+  }
+  std::sort(need.begin(), need.end());
+  need.erase(std::unique(need.begin(), need.end()), need.end());
+  std::vector<cel::Object> parsed(need.size());
+  const std::string& text = *w.cav.text;
+  const std::vector<uint32_t>& off = *w.cav.off;
+  host_parallel(need.size(), 512, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t s = need[k];
+      parsed[k] = cel::parse_context(text.substr(off[s - 1], off[s] - off[s - 1]));
+    }
+  });
+  for (size_t k = 0; k < need.size(); ++k) w.cav_parsed.emplace(need[k], std::move(parsed[k]));
+  std::vector<uint8_t> out(keys.size());
+  host_parallel(keys.size(), 256, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t row = (uint32_t)(keys[k] >> 32), slot = (uint32_t)keys[k];
+      const uint32_t id = e.caveat_partial[row];
+      const cel::Object& ctx = w.cav_parsed.at(slot);
+      try {
+        out[k] = (uint8_t)cel::evaluate(*e.caveat_expr[id], &e.caveat_ctx[id], &ctx);
+      } catch (const Error&) {
+        out[k] = 3;
+      }
+    }
+  });
+  const size_t n = keys.size();
+  for (size_t k = 0; k < n; ++k) w.cav_eval[keys[k]] = out[k];
+  std::lock_guard<std::mutex> lk(e.stats_mu);
+  e.stats.caveat_evals += n;
 }
 
 // ---- batches ---------------------------------------------------------------------------------
@@ -2089,6 +2309,7 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   w.b_dperm = host ? w.d_perm : perm;
   w.b_derr = host ? w.d_err : err;
   w.b_ms = 0.f;
+  w.b_cav_req = w.b_cav_err = 0;
   w.fail_code = 0;
   w.fail_msg.clear();
   if (host) {
@@ -2104,13 +2325,70 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
     w.b_xperm = pin_out ? perm : w.h_perm;
     w.b_xerr = pin_out ? err : w.h_err;
   }
-  if (e.cfg.flags & GCK_FLAG_NO_BUNDLE) {
-    w.b_bundles = false;
-  } else {
-    w.b_bundles = true;
-    bundles_launch(e, w, w.b_items, n, now_us, w.b_dperm, w.b_derr, w.b_st, host);
-  }
+  if (w.cav_on) HIP_OK(hipMemsetAsync(w.cav_flag, 0, n, w.b_st));
+  w.b_bundles = !(e.cfg.flags & GCK_FLAG_NO_BUNDLE);
+  if (w.b_bundles) bundles_launch(e, w, w.b_items, n, now_us, w.b_dperm, w.b_derr, w.b_st, host);
   w.state = 1;
+}
+
+// The rest of a pass whose stage A is queued (bundle path), or the whole pass (grid-wide path).
+static float finish_pass(Engine& e, Workspace& w) {
+  const bool host = w.b_hperm != nullptr;
+  if (w.b_bundles) return bundles_finish(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, host);
+  float ms = 0.f;
+  check_range_wide(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, &ms);
+  if (host) {
+    HIP_OK(hipMemcpyAsync(w.b_xperm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, w.b_st));
+    HIP_OK(hipMemcpyAsync(w.b_xerr, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, w.b_st));
+    HIP_OK(hipStreamSynchronize(w.b_st));
+  }
+  return ms;
+}
+
+// Lazy caveat evaluation after a pass: while the pass met pairs not evaluated yet, evaluate the
+// ones it recorded and run the batch again (the walk of every check is repeated; a pass that
+// sees only evaluated pairs is exact). Then the checks that touched a failing pair get their
+// item error.
+static void caveat_passes(Engine& e, Workspace& w) {
+  const hipStream_t st = w.b_st;
+  for (uint32_t pass = 0; w.cav_lazy && w.b_cav_req > 0; ++pass) {
+    // each pass evaluates at least one new pair (one a pass met unevaluated is recorded unless
+    // the list is full, and a full list holds kReqCap new pairs)
+    if (pass > 4096) throw Error(GCK_E_DEVICE, "engine invariant violated: caveat passes do not settle");
+    unsigned cnt = 0;
+    HIP_OK(hipMemcpyAsync(&cnt, w.req_cnt, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    cnt = std::min(cnt, kReqCap);
+    if (cnt == 0) throw Error(GCK_E_DEVICE, "engine invariant violated: caveat pairs met but none recorded");
+    std::vector<unsigned long long> keys(cnt);
+    HIP_OK(hipMemcpyAsync(keys.data(), w.req_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (unsigned long long k : keys) {
+      const uint32_t row = (uint32_t)(k >> 32), slot = (uint32_t)k;
+      if (row >= e.caveat_partial.size() || slot == 0 || slot > w.cav.n_ctx || w.cav_eval.count(k))
+        throw Error(GCK_E_DEVICE, "engine invariant violated: caveat pair request");
+    }
+    evaluate_pairs(e, w, keys);
+    upload_cav_map(w, st);
+    HIP_OK(hipMemsetAsync(w.req_set, 0xFF, (size_t)kReqSet * 8, st));
+    HIP_OK(hipMemsetAsync(w.req_cnt, 0, 4, st));
+    HIP_OK(hipMemsetAsync(w.cav_flag, 0, w.b_n, st));
+    w.b_cav_req = w.b_cav_err = 0;
+    if (w.b_bundles)
+      bundles_launch(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, st, w.b_hperm != nullptr);
+    w.b_ms += finish_pass(e, w);
+    std::lock_guard<std::mutex> lk(e.stats_mu);
+    e.stats.caveat_passes++;
+  }
+  if (w.b_cav_err == 0) return;
+  hipLaunchKernelGGL(k_cav_fail, dim3((w.b_n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, w.cav_flag, w.b_n,
+                     w.b_dperm, w.b_derr);
+  HIP_OK(hipGetLastError());
+  if (w.b_hperm) {
+    HIP_OK(hipMemcpyAsync(w.b_xperm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(w.b_xerr, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
 }
 
 // Completes the batch in flight (caller holds w.m). The results are in the caller's device
@@ -2118,16 +2396,8 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
 static void finish_batch(Engine& e, Workspace& w) {
   if (w.state != 1) return;
   w.state = 2;
-  if (w.b_bundles) {
-    w.b_ms = bundles_finish(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, w.b_hperm != nullptr);
-  } else {
-    check_range_wide(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, w.b_st, &w.b_ms);
-    if (w.b_hperm) {
-      HIP_OK(hipMemcpyAsync(w.b_xperm, w.b_dperm, w.b_n, hipMemcpyDeviceToHost, w.b_st));
-      HIP_OK(hipMemcpyAsync(w.b_xerr, w.b_derr, (size_t)w.b_n * 4, hipMemcpyDeviceToHost, w.b_st));
-      HIP_OK(hipStreamSynchronize(w.b_st));
-    }
-  }
+  w.b_ms = finish_pass(e, w);
+  if (w.cav_on) caveat_passes(e, w);
 }
 
 static void copy_out(Workspace& w) {
@@ -2156,13 +2426,13 @@ void drain_batches(Engine& e) {
 }
 
 void device_check(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm,
-                  int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
+                  int32_t* d_err, void* stream, CavCall cav) {
   HIP_OK(hipSetDevice(e.device));
   std::lock_guard<std::mutex> lk(w.m);
   // the caller's stream; NULL is the legacy default stream (never the workspace's own
   // non-blocking stream, which would not be ordered after the caller's writes of the items)
   hipStream_t st = (hipStream_t)stream;
-  stage_caveats(w, cav_table, n_ctx, st);
+  stage_caveats(w, std::move(cav), st);
   if (now_us == 0) now_us = wall_now_us();
   float ms = 0.f;
   for (size_t pos = 0; pos < n; pos += w.max_batch) {
@@ -2179,7 +2449,7 @@ void device_check(Engine& e, Workspace& w, const gck_item* d_items, size_t n, in
 // Host buffers: chunks of max_batch on two workspaces in turn, so that a chunk's copies and
 // host staging overlap the previous chunk's kernels.
 void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* items, size_t n, int64_t now_us,
-                       uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
+                       uint8_t* perm, int32_t* err, const CavCall& cav) {
   HIP_OK(hipSetDevice(e.device));
   if (now_us == 0) now_us = wall_now_us();
   const size_t mb = w0->max_batch;
@@ -2188,7 +2458,8 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
   std::lock_guard<std::mutex> g0(ws[0]->m);
   std::unique_ptr<std::lock_guard<std::mutex>> g1;
   if (ws[1] != ws[0]) g1.reset(new std::lock_guard<std::mutex>(ws[1]->m));
-  for (Workspace* w : {ws[0], ws[1]}) stage_caveats(*w, cav_table, n_ctx, w->stream);
+  stage_caveats(*ws[0], CavCall(cav), ws[0]->stream);
+  if (ws[1] != ws[0]) stage_caveats(*ws[1], CavCall(cav), ws[1]->stream);
   float ms = 0.f;
   Workspace* prev = nullptr;
   for (size_t k = 0; k < n_chunks; ++k) {
@@ -2215,12 +2486,12 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
 }
 
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                   int32_t* err, void* stream, bool host, const std::vector<uint8_t>& cav_table, uint32_t n_ctx) {
+                   int32_t* err, void* stream, bool host, CavCall cav) {
   HIP_OK(hipSetDevice(e.device));
   std::lock_guard<std::mutex> lk(w->m);
   if (n > w->max_batch) throw Error(GCK_E_INVALID_ARGUMENT, "submitted batch above max_batch");
   hipStream_t st = host ? w->stream : (hipStream_t)stream;
-  stage_caveats(*w, cav_table, n_ctx, st);
+  stage_caveats(*w, std::move(cav), st);
   if (now_us == 0) now_us = wall_now_us();
   submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host);
 }

@@ -132,6 +132,23 @@ struct UpdateGroup {
   std::vector<int64_t> exp_us;           // expiration per key (0 = never)
 };
 
+// The check-time caveat contexts of one call (CheckBulkPermissionsRequestItem.Context,
+// client/client.go:257) and how their outcomes reach the device: a dense table of every partial
+// caveat instance x context when that is small, otherwise lazily — the walk records the pairs it
+// touches, the host parses and evaluates just those and the batch runs again (engine.hip
+// caveat_passes).
+struct CavCall {
+  uint32_t n_ctx = 0;             // contexts of the call (0: none, or no partial instance)
+  // dense: rows x n_dist outcomes (0 false, 1 true, 2 partial, 3 error) over the distinct
+  // context texts, and each slot's distinct text; empty with n_ctx > 0: lazy
+  std::vector<uint8_t> dense;
+  uint32_t n_dist = 0;
+  std::vector<uint32_t> of_slot;
+  // lazy: the contexts' JSON texts, concatenated (slot k + 1 = [off[k], off[k + 1]))
+  std::shared_ptr<const std::string> text;
+  std::shared_ptr<const std::vector<uint32_t>> off;
+};
+
 struct DeviceSnapshot;  // engine.hip
 struct Workspace;       // engine.hip
 
@@ -201,8 +218,7 @@ int device_init(Engine& e);
 // previous heights are taken over
 void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta = false);
 void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
-// cav_table: the call's caveat outcome table (row = partial instance, n_ctx columns = check
-// contexts 1..n_ctx; empty when the call has no check contexts)
+// cav: the call's check-time caveat contexts (CavCall above)
 // Pooled check workspaces (one per batch in flight, at most cfg.workspaces): acquire waits for
 // a free one. Callers take their workspaces BEFORE the engine lock (the holders of busy ones
 // may need the lock to finish their batches).
@@ -217,17 +233,16 @@ struct WsLease {
   WsLease& operator=(const WsLease&) = delete;
 };
 void device_check(Engine& e, Workspace& w, const gck_item* d_items, size_t n, int64_t now_us,
-                  uint8_t* d_perm, int32_t* d_err, void* stream, const std::vector<uint8_t>& cav_table,
-                  uint32_t n_ctx);
+                  uint8_t* d_perm, int32_t* d_err, void* stream, CavCall cav);
 // Host buffers, chunks of max_batch alternating over w0 and w1 (w1 may be null or w0).
 void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* items, size_t n, int64_t now_us,
-                       uint8_t* perm, int32_t* err, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
+                       uint8_t* perm, int32_t* err, const CavCall& cav);
 // Asynchronous batches (gck_check_submit / gck_check_wait): submit starts one batch (n <=
 // max_batch) on an acquired workspace; wait finishes it (later stages, results copied out) —
 // the caller then releases the workspace. `items` etc. are device pointers on `stream`
 // (host == false) or host buffers (host == true: the workspace's own stream).
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                   int32_t* err, void* stream, bool host, const std::vector<uint8_t>& cav_table, uint32_t n_ctx);
+                   int32_t* err, void* stream, bool host, CavCall cav);
 void device_wait(Engine& e, Workspace* w);
 // Pinned host buffers (gck_host_alloc): a host batch whose items / results live in one is
 // copied by DMA directly, without the workspace's staging copy.

@@ -2,6 +2,7 @@
 // exceptions into a negative status plus a thread-local message (gck_last_error).
 #include <cstring>
 #include <string>
+#include <string_view>
 
 #include "engine.hpp"
 
@@ -55,33 +56,67 @@ uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::stri
   return id;
 }
 
-// The outcome table of one check call: row r = partial instance caveat_partial[r], column k =
-// check context k + 1 (CheckBulkPermissionsRequestItem.Context, client/client.go:257), each
-// merged under the instance's stored context. Identical context texts share a column's
-// evaluation.
-static std::vector<uint8_t> caveat_table(Engine& e, const char* const* ctxs, const size_t* lens, size_t n_ctx) {
-  std::vector<uint8_t> t;
+// The check-time caveat contexts of one call (engine.hpp CavCall). Each partial instance r
+// (caveat_partial[r]) under context slot k + 1 (CheckBulkPermissionsRequestItem.Context,
+// client/client.go:257) is evaluated with the instance's stored context taking precedence.
+// While instances x contexts is small every pair is evaluated here into a dense table (identical
+// context texts share their evaluations); beyond that the contexts are only copied, and the pairs
+// a walk touches are parsed and evaluated on demand (engine.hip caveat_passes). An evaluation
+// error is outcome 3: it fails only the checks whose walk meets it (GCK_ITEM_ERR_CAVEAT_EVAL).
+constexpr size_t kDensePairs = 4096;  // evaluations done eagerly
+
+static CavCall caveat_call(Engine& e, const char* const* ctxs, const size_t* lens, size_t n_ctx) {
+  CavCall c;
   const size_t rows = e.caveat_partial.size();
-  if (n_ctx == 0 || rows == 0) return t;
-  REQUIRE(rows * n_ctx <= (1ull << 30), GCK_E_CAPACITY,
-          "caveat outcome table too large (partial caveat instances x check contexts)");
-  t.resize(rows * n_ctx);
-  std::unordered_map<std::string, size_t> seen;
-  for (size_t k = 0; k < n_ctx; ++k) {
-    std::string js(ctxs[k] ? ctxs[k] : "", ctxs[k] ? lens[k] : 0);
-    auto it = seen.find(js);
-    if (it != seen.end()) {
-      for (size_t r = 0; r < rows; ++r) t[r * n_ctx + k] = t[r * n_ctx + it->second];
-      continue;
+  if (n_ctx == 0 || rows == 0) return c;
+  REQUIRE(n_ctx < (1ull << 31), GCK_E_INVALID_ARGUMENT, "too many check contexts");
+  c.n_ctx = (uint32_t)n_ctx;
+  if (!(e.cfg.flags & GCK_FLAG_LAZY_CAVEATS) && rows <= kDensePairs) {
+    std::unordered_map<std::string_view, uint32_t> seen;
+    seen.reserve(std::min<size_t>(n_ctx, 4 * kDensePairs));
+    std::vector<std::string_view> dist;
+    c.of_slot.resize(n_ctx);
+    for (size_t k = 0; k < n_ctx && rows * dist.size() <= kDensePairs; ++k) {
+      const std::string_view js(ctxs[k] ? ctxs[k] : "", ctxs[k] ? lens[k] : 0);
+      auto it = seen.emplace(js, (uint32_t)dist.size()).first;
+      if (it->second == dist.size()) dist.push_back(js);
+      c.of_slot[k] = it->second;
     }
-    const cel::Object ctx = cel::parse_context(js);
-    for (size_t r = 0; r < rows; ++r) {
-      const uint32_t id = e.caveat_partial[r];
-      t[r * n_ctx + k] = (uint8_t)cel::evaluate(*e.caveat_expr[id], &e.caveat_ctx[id], &ctx);
+    if (rows * dist.size() <= kDensePairs) {
+      const size_t nd = dist.size();
+      c.n_dist = (uint32_t)nd;
+      c.dense.resize(rows * nd);
+      for (size_t k = 0; k < nd; ++k) {
+        const cel::Object ctx = cel::parse_context(std::string(dist[k]));  // a malformed context fails the call
+        for (size_t r = 0; r < rows; ++r) {
+          const uint32_t id = e.caveat_partial[r];
+          try {
+            c.dense[r * nd + k] = (uint8_t)cel::evaluate(*e.caveat_expr[id], &e.caveat_ctx[id], &ctx);
+          } catch (const Error&) {
+            c.dense[r * nd + k] = 3;
+          }
+        }
+      }
+      return c;
     }
-    seen.emplace(std::move(js), k);
+    c.of_slot.clear();
   }
-  return t;
+  // lazy: one copy of the texts (a context is parsed when a walk first needs it; a malformed one
+  // then fails the call)
+  size_t total = 0;
+  for (size_t k = 0; k < n_ctx; ++k) total += ctxs[k] ? lens[k] : 0;
+  REQUIRE(total < (1ull << 32), GCK_E_INVALID_ARGUMENT, "check contexts above 4 GiB");
+  auto text = std::make_shared<std::string>();
+  auto off = std::make_shared<std::vector<uint32_t>>(n_ctx + 1);
+  text->reserve(total);
+  for (size_t k = 0; k < n_ctx; ++k) {
+    (*off)[k] = (uint32_t)text->size();
+    if (ctxs[k]) text->append(ctxs[k], lens[k]);
+  }
+  (*off)[n_ctx] = (uint32_t)text->size();
+  c.text = std::move(text);
+  c.off = std::move(off);
+  return c;
 }
 
 void stage_tuple(Engine& e, const gck_tuple& t);
@@ -126,7 +161,7 @@ static Schema& need_schema(Engine& e) {
 extern "C" {
 
 static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
-static_assert(sizeof(gck_stats) == 192, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
+static_assert(sizeof(gck_stats) == 208, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32 && sizeof(gck_update) == 40, "item/tuple/update layout");
 
 int gck_abi_version(void) { return GCK_ABI_VERSION; }
@@ -572,8 +607,8 @@ int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item
     if (n > mb) l1.reset(new WsLease(e));
     std::shared_lock<std::shared_mutex> lk(e.mu);
     check_request(e, cs, items, n, true, contexts, context_lens, n_contexts);
-    const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
-    device_check_host(e, l0.w, l1 ? l1->w : nullptr, items, n, now_us, out_perm, out_err, table, (uint32_t)n_contexts);
+    const CavCall cav = caveat_call(e, contexts, context_lens, n_contexts);
+    device_check_host(e, l0.w, l1 ? l1->w : nullptr, items, n, now_us, out_perm, out_err, cav);
   });
 }
 
@@ -597,8 +632,8 @@ int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n,
     WsLease l0(e);
     std::shared_lock<std::shared_mutex> lk(e.mu);
     check_request(e, nullptr, nullptr, 0, false, contexts, context_lens, n_contexts);
-    const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
-    device_check(e, *l0.w, d_items, n, now_us, d_out_perm, d_out_err, stream, table, (uint32_t)n_contexts);
+    device_check(e, *l0.w, d_items, n, now_us, d_out_perm, d_out_err, stream,
+                 caveat_call(e, contexts, context_lens, n_contexts));
   });
 }
 
@@ -639,8 +674,8 @@ int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* 
     try {
       std::shared_lock<std::shared_mutex> lk(e.mu);
       check_request(e, cs, items, n, host, contexts, context_lens, n_contexts);
-      const std::vector<uint8_t> table = caveat_table(e, contexts, context_lens, n_contexts);
-      device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host, table, (uint32_t)n_contexts);
+      device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host,
+                    caveat_call(e, contexts, context_lens, n_contexts));
     } catch (...) {
       release_ws(e, w);
       delete b;

@@ -38,6 +38,7 @@ ITEM_ERR_UNKNOWN_PERMISSION = 2
 ITEM_ERR_UNKNOWN_TYPE = 3
 ITEM_ERR_UNKNOWN_SUBJECT_RELATION = 4
 ITEM_ERR_WILDCARD_SUBJECT = 5
+ITEM_ERR_CAVEAT_EVAL = 6
 
 ELLIPSIS = 0xFFFF
 ID_WILDCARD = 0xFFFFFFFF
@@ -55,6 +56,7 @@ FLAG_NO_MHASH = 4
 FLAG_NO_GIANT = 8
 FLAG_NO_BIDIR = 16
 FLAG_NO_CLOSURE = 32
+FLAG_LAZY_CAVEATS = 64
 SUBMIT_DEVICE = 1
 
 ITEM_DTYPE = np.dtype([
@@ -82,6 +84,7 @@ ITEM_ERROR_MESSAGES = {
     ITEM_ERR_UNKNOWN_TYPE: "object definition not found",
     ITEM_ERR_UNKNOWN_SUBJECT_RELATION: "subject relation not found",
     ITEM_ERR_WILDCARD_SUBJECT: "cannot perform check on wildcard subject",
+    ITEM_ERR_CAVEAT_EVAL: "evaluation error for caveat",
 }
 
 
@@ -118,7 +121,8 @@ class _Stats(C.Structure):
                 ("edges_launches", C.c_uint64), ("bundle_ms", C.c_double),
                 ("bundle_launches", C.c_uint64), ("deferred", C.c_uint64),
                 ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64),
-                ("bidir_checks", C.c_uint64), ("bundles", C.c_uint64), ("closure_checks", C.c_uint64)]
+                ("bidir_checks", C.c_uint64), ("bundles", C.c_uint64), ("closure_checks", C.c_uint64),
+                ("caveat_evals", C.c_uint64), ("caveat_passes", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -236,11 +240,13 @@ class Engine:
                  bundle_visited: int = 0, bundle_waves_per_cu: int = 0,
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
                  giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
-                 bidir: bool = True, bidir_both: int = 0, workspaces: int = 0, closure: bool = True):
+                 bidir: bool = True, bidir_both: int = 0, workspaces: int = 0, closure: bool = True,
+                 lazy_caveats: bool = False):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
                  | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
-                 | (0 if bidir else FLAG_NO_BIDIR) | (0 if closure else FLAG_NO_CLOSURE))
+                 | (0 if bidir else FLAG_NO_BIDIR) | (0 if closure else FLAG_NO_CLOSURE)
+                 | (FLAG_LAZY_CAVEATS if lazy_caveats else 0))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,
@@ -647,13 +653,26 @@ def _context_json(ctx) -> str:
     return json.dumps(ctx, sort_keys=True, separators=(",", ":"))
 
 
+class Contexts:
+    """Check-time caveat contexts marshalled once for the C ABI (the `contexts` / `context_lens`
+    arrays of gck_check_bulk_ctx): pass it wherever `contexts` is taken to reuse the arrays
+    across calls (a caller that builds its requests ahead, as a Go caller's slices are)."""
+
+    def __init__(self, contexts):
+        self._enc = [_context_json(c).encode() for c in contexts]
+        self.arr = (C.c_char_p * len(self._enc))(*self._enc)
+        self.lens = (C.c_size_t * len(self._enc))(*[len(b) for b in self._enc])
+
+    def __len__(self):
+        return len(self._enc)
+
+
 def _context_arrays(contexts):
-    if not contexts:
+    if contexts is None or len(contexts) == 0:
         return None, None, 0
-    enc = [_context_json(c).encode() for c in contexts]
-    arr = (C.c_char_p * len(enc))(*enc)
-    lens = (C.c_size_t * len(enc))(*[len(b) for b in enc])
-    return arr, lens, len(enc)
+    if not isinstance(contexts, Contexts):
+        contexts = Contexts(contexts)
+    return contexts.arr, contexts.lens, len(contexts)
 
 
 PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES

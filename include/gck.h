@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 5
+#define GCK_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -85,6 +85,8 @@ extern "C" {
 #define GCK_ITEM_ERR_UNKNOWN_TYPE 3             /* resource or subject type not defined */
 #define GCK_ITEM_ERR_UNKNOWN_SUBJECT_RELATION 4 /* subject relation not defined */
 #define GCK_ITEM_ERR_WILDCARD_SUBJECT 5         /* subject id "*" is not checkable */
+#define GCK_ITEM_ERR_CAVEAT_EVAL 6              /* a caveat on the check's walk failed to evaluate
+                                                   under its context (a type error, a bad value) */
 
 /* ---- special ids ---------------------------------------------------------------------- */
 #define GCK_ELLIPSIS 0xFFFFu          /* subject relation "..." (a concrete object) */
@@ -108,6 +110,9 @@ extern "C" {
 #define GCK_FLAG_NO_BIDIR 16u    /* gck_config.flags: forward-only search (no bidirectional checks) */
 #define GCK_FLAG_NO_CLOSURE 32u  /* gck_config.flags: no closure-join stage (nested-group checks take
                                     the bundle search) */
+#define GCK_FLAG_LAZY_CAVEATS 64u /* gck_config.flags: always evaluate check-time caveat contexts
+                                     lazily (only the pairs a walk meets; by default a call whose
+                                     partial instances x distinct contexts is small evaluates them all) */
 
 typedef struct gck_engine gck_engine;
 
@@ -203,6 +208,8 @@ typedef struct gck_stats {
   uint64_t bundles;            /* check bundles run by the bundle kernels (`levels` also sums
                                   their BFS levels) */
   uint64_t closure_checks;     /* checks answered by the closure-join stage (nested groups) */
+  uint64_t caveat_evals;       /* (caveat instance, check context) pairs evaluated on the host */
+  uint64_t caveat_passes;      /* extra batch passes after lazily evaluated caveat pairs */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
@@ -291,9 +298,12 @@ int gck_check_bulk(gck_engine* e, const gck_consistency* cs, const gck_item* ite
 /* Same, with check-time caveat contexts: contexts[k] (JSON object text, context_lens[k] bytes)
  * is the context of every item whose context_slot is k + 1. A caveat is evaluated over its
  * stored context merged with the item's context (stored values take precedence): true = the
- * relationship counts, false = it does not, missing parameter = CONDITIONAL.
- * Errors: GCK_E_INVALID_ARGUMENT (a context_slot > n_contexts, malformed JSON, a CEL evaluation
- * error), GCK_E_CAPACITY (partial caveat instances x contexts above 2^30). */
+ * relationship counts, false = it does not, missing parameter = CONDITIONAL. Only the
+ * (caveat instance, context) pairs the checks' walks meet are evaluated once the product of
+ * partial instances and distinct contexts is large (the batch then runs again with their
+ * outcomes); a pair that fails to evaluate gives the items whose walk met it
+ * GCK_ITEM_ERR_CAVEAT_EVAL and nothing else.
+ * Errors: GCK_E_INVALID_ARGUMENT (a context_slot > n_contexts, malformed JSON). */
 int gck_check_bulk_ctx(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
                        const char* const* contexts, const size_t* context_lens, size_t n_contexts,
                        int64_t now_us, uint8_t* out_perm, int32_t* out_err);

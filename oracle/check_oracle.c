@@ -12,7 +12,10 @@
  *                                                                         §5.1 items 4-6
  * Tri-state algebra as spicedb_ref.py: union Y > ERR > C > N; intersection N > ERR > C > Y;
  * exclusion N if base N or a subtracted Y, else ERR, else C, else Y. Caveated edges are
- * CONDITIONAL (the device contract: CEL runs on the host afterwards).
+ * CONDITIONAL, except under orc_check_quota, which restates one caveat family in C — the
+ * threshold `value < limit` (limit stored per relationship, value per check context) — so that
+ * large per-relationship x per-request caveat workloads have a scale checker; a caveat that
+ * fails to evaluate on a check's walk makes the item GCK_ITEM_ERR_CAVEAT_EVAL (6).
  *
  * Parity pinning: cross-checked against spicedb_ref.py (itself pinned by the reference's
  * known answers, tests/golden) on seeded graphs in tests/test_c_oracle.py.
@@ -74,6 +77,13 @@ typedef struct {
   const orc_csr* csrs;
   int64_t now_us;
   int max_depth;
+  /* threshold caveats (orc_check_quota): edge cav id k > 0 holds while the check's value is
+     below limit[k]; the value of context slot s is used[s - 1] (INT64_MIN: the context gives the
+     parameter a wrong type, an evaluation error); slot 0 leaves the caveat unresolved. NULL
+     limit: every caveated edge is unresolved (CONDITIONAL). */
+  const int64_t* cav_limit;
+  const int64_t* cav_used;
+  uint32_t n_slots;
 } orc_program;
 
 typedef struct {
@@ -87,6 +97,8 @@ typedef struct {
   /* subject */
   uint32_t sid;
   uint16_t stype, srel;
+  uint32_t slot;  /* the check's context slot */
+  int cav_err;    /* the walk met a caveat that failed to evaluate */
   uint64_t rows, probes, edges;
 } orc_ctx;
 
@@ -97,10 +109,11 @@ static int union3(int a, int b) {
   return NO;
 }
 
-static int and3(int cav, int sub) { /* caveated edge conditions what it reaches */
+/* a caveated edge conditions what it reaches: spicedb_ref.and3 over the caveat's outcome */
+static int and3(int cav, int sub) {
   if (sub == ERR) return ERR;
-  if (!cav) return sub;
-  if (sub == NO) return NO;
+  if (cav == HAS) return sub;
+  if (cav == NO || sub == NO) return NO;
   return COND;
 }
 
@@ -175,6 +188,19 @@ static int visible(const orc_program* p, const orc_csr* r, uint32_t pos) {
   return !r->exp || r->exp[pos] == 0 || r->exp[pos] > p->now_us;
 }
 
+/* the outcome of edge pos's caveat for the current check: HAS (no caveat, or it holds), NO
+   (it fails) or COND (unresolved) */
+static int cav_at(const orc_program* p, orc_ctx* c, const orc_csr* r, uint32_t pos) {
+  if (!r->cav || !r->cav[pos]) return HAS;
+  if (!p->cav_limit || c->slot == 0 || c->slot > p->n_slots) return COND;
+  int64_t u = p->cav_used[c->slot - 1];
+  if (u == INT64_MIN) {
+    c->cav_err = 1;
+    return COND;
+  }
+  return u < p->cav_limit[r->cav[pos]] ? HAS : NO;
+}
+
 static int dispatch(const orc_program* p, orc_ctx* c, int type, uint32_t obj, int rel, int dr);
 
 static int computed(const orc_program* p, orc_ctx* c, int type, uint32_t obj, int rel, int dr) {
@@ -200,7 +226,7 @@ static int check_direct(const orc_program* p, orc_ctx* c, int rel, uint32_t obj,
       const orc_csr* r = &p->csrs[ci];
       uint32_t pos;
       if (direct && row_find(c, r, obj, c->sid, &pos) && visible(p, r, pos)) {
-        int v = and3(r->cav && r->cav[pos], HAS);
+        int v = and3(cav_at(p, c, r, pos), HAS);
         acc = union3(acc, v);
         if (acc == HAS) return HAS;
       }
@@ -208,7 +234,7 @@ static int check_direct(const orc_program* p, orc_ctx* c, int rel, uint32_t obj,
         uint32_t b = r->off[obj], e = r->off[obj + 1];
         c->probes++;
         if (e > b && r->nbr[e - 1] == WILDCARD && visible(p, r, e - 1)) {
-          acc = union3(acc, and3(r->cav && r->cav[e - 1], HAS));
+          acc = union3(acc, and3(cav_at(p, c, r, e - 1), HAS));
           if (acc == HAS) return HAS;
         }
       }
@@ -230,7 +256,7 @@ static int check_direct(const orc_program* p, orc_ctx* c, int rel, uint32_t obj,
         uint32_t x = r->nbr[e];
         if (x == WILDCARD) continue;
         int sub = dispatch(p, c, stype, x, srel, dr - 1);
-        acc = union3(acc, and3(r->cav && r->cav[e], sub));
+        acc = union3(acc, and3(cav_at(p, c, r, e), sub));
         if (acc == HAS) return HAS;
       }
     }
@@ -336,7 +362,7 @@ static int eval(const orc_program* p, orc_ctx* c, const int32_t** pc, int type, 
           for (uint32_t e = r->off[obj]; e < r->off[obj + 1]; ++e) {
             c->edges++;
             if (!visible(p, r, e)) continue;
-            int v = and3(r->cav && r->cav[e], computed(p, c, stype, r->nbr[e], target, dr));
+            int v = and3(cav_at(p, c, r, e), computed(p, c, stype, r->nbr[e], target, dr));
             seen = 1;
             if (is_all) {
               if (v == NO) return NO;
@@ -384,10 +410,14 @@ static int validate(const orc_program* p, const orc_item* it) {
 }
 
 /* Program layout: [n_types, n_rels, rel_off[n_rels]..., records...]. */
-int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, size_t n,
-              int64_t now_us, int max_depth, int threads, uint8_t* out_perm, int32_t* out_err,
-              uint64_t* counters /* [rows, probes, edges] or NULL */) {
+int orc_check_quota(const int32_t* prog, const orc_csr* csrs, const orc_item* items, size_t n,
+                    int64_t now_us, int max_depth, int threads, uint8_t* out_perm, int32_t* out_err,
+                    uint64_t* counters /* [rows, probes, edges] or NULL */, const int64_t* cav_limit,
+                    const int64_t* cav_used, uint32_t n_slots) {
   orc_program p;
+  p.cav_limit = cav_limit;
+  p.cav_used = cav_used;
+  p.n_slots = n_slots;
   p.n_types = prog[0];
   p.n_rels = prog[1];
   p.rel_at = prog + 2;
@@ -428,8 +458,12 @@ int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, s
       c.sid = it->subject_id;
       c.stype = it->subject_type;
       c.srel = it->subject_relation;
+      c.slot = it->context_slot;
+      c.cav_err = 0;
       int v = dispatch(&p, &c, it->resource_type, it->resource_id, it->permission, p.max_depth);
-      if (v == ERR) {
+      if (c.cav_err) {
+        out_err[i] = 6; /* GCK_ITEM_ERR_CAVEAT_EVAL */
+      } else if (v == ERR) {
         out_err[i] = 1;
       } else {
         out_perm[i] = (uint8_t)v;
@@ -450,6 +484,13 @@ int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, s
     counters[2] = edges;
   }
   return 0;
+}
+
+int orc_check(const int32_t* prog, const orc_csr* csrs, const orc_item* items, size_t n,
+              int64_t now_us, int max_depth, int threads, uint8_t* out_perm, int32_t* out_err,
+              uint64_t* counters) {
+  return orc_check_quota(prog, csrs, items, n, now_us, max_depth, threads, out_perm, out_err, counters, NULL,
+                         NULL, 0);
 }
 
 /*

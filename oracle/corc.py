@@ -49,6 +49,8 @@ def lib():
         l.orc_check.restype = C.c_int
         l.orc_check.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int64, C.c_int,
                                 C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        l.orc_check_quota.restype = C.c_int
+        l.orc_check_quota.argtypes = l.orc_check.argtypes + [C.c_void_p, C.c_void_p, C.c_uint32]
         l.orc_count_bfs.restype = C.c_int
         l.orc_count_bfs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int,
                                     C.c_void_p]
@@ -235,6 +237,25 @@ def check(program: np.ndarray, csr_table, items: np.ndarray, now_us: int = 0, ma
     lib().orc_check(program.ctypes.data, C.addressof(tab), items.ctypes.data, n, now_us, max_depth,
                     threads, perm.ctypes.data, err.ctypes.data, ctr.ctypes.data)
     return perm, err, dict(rows=int(ctr[0]), probes=int(ctr[1]), edges=int(ctr[2]))
+
+
+def check_quota(program: np.ndarray, csr_table, items: np.ndarray, limits: np.ndarray, used: np.ndarray,
+                now_us: int = 0, max_depth: int = 50, threads: int = 1):
+    """check() with threshold caveats: caveated edge k holds while the check's value
+    used[context_slot - 1] is below limits[k] (INT64_MIN: an evaluation error; slot 0:
+    unresolved). Returns (perm, err)."""
+    tab, _keep = csr_table
+    items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
+    program = np.ascontiguousarray(program, dtype=np.int32)
+    limits = np.ascontiguousarray(limits, dtype=np.int64)
+    used = np.ascontiguousarray(used, dtype=np.int64)
+    n = len(items)
+    perm = np.zeros(n, dtype=np.uint8)
+    err = np.zeros(n, dtype=np.int32)
+    lib().orc_check_quota(program.ctypes.data, C.addressof(tab), items.ctypes.data, n, now_us, max_depth,
+                          threads, perm.ctypes.data, err.ctypes.data, None, limits.ctypes.data,
+                          used.ctypes.data, len(used))
+    return perm, err
 
 
 def count_bfs(program: np.ndarray, csr_table, items: np.ndarray, threads: int = 1):

@@ -59,6 +59,7 @@ ITEM_ERR_UNKNOWN_PERMISSION = 2
 ITEM_ERR_UNKNOWN_TYPE = 3
 ITEM_ERR_UNKNOWN_SUBJECT_RELATION = 4
 ITEM_ERR_WILDCARD_SUBJECT = 5
+ITEM_ERR_CAVEAT_EVAL = 6  # a caveat met by the check failed to evaluate under its context
 
 DEFAULT_MAX_DEPTH = 50
 
@@ -1009,7 +1010,12 @@ class Checker:
         # context and clock, _dispatch is a pure function of its arguments, so this changes no
         # result — it only keeps cyclic and re-converging data polynomial (|vertices| x depth).
         self._memo = {}
-        r = self._dispatch(it.resource_type, it.resource_id, it.permission, self.max_depth)
+        try:
+            r = self._dispatch(it.resource_type, it.resource_id, it.permission, self.max_depth)
+        except SchemaError:
+            raise
+        except (ValueError, TypeError):  # cel_eval: a caveat failed on the merged context (CEL type errors)
+            return 0, ITEM_ERR_CAVEAT_EVAL
         if r == ERR:
             return 0, ITEM_ERR_MAX_DEPTH
         return r, ITEM_OK

@@ -412,3 +412,96 @@ class Mixed:
         items.view(torch.int32).reshape(n, 5)[:, 4] = slot
         return items
 
+
+
+# ---- config 5 variant: per-relationship and per-request caveat contexts ---------------------
+
+QUOTA_SCHEMA = MIXED_SCHEMA.replace(
+    'caveat only_on_tuesday(day_of_the_week string) {\n  day_of_the_week == "tuesday"\n}',
+    "caveat quota(limit int, used int) {\n  used < limit\n}").replace("only_on_tuesday", "quota")
+BAD_USED = np.iinfo(np.int64).min  # corc.check_quota: the context gives `used` a wrong type
+
+
+class Quota(Mixed):
+    """BASELINE config 5 with realistic caveat contexts: the config-2 graph with 10 % of the
+    folder / doc viewer and editor user tuples caveated ``with quota``, each relationship storing
+    its own ``{"limit": L}`` (L from `n_limits` distinct values, so that many partial caveat
+    instances), and every check carrying its own ``{"used": U}`` (one context per request; 10 %
+    carry none and stay CONDITIONAL). The caveat holds when U < L: the outcome depends on the
+    (instance, context) pair, which the C oracle's threshold mode (corc.check_quota) restates."""
+
+    def __init__(self, scale: float = 1.0, seed: int = 20251003, device="cuda", cav_frac: float = 0.1,
+                 n_limits: int = 32768):
+        super().__init__(scale, seed, device, cav_frac)
+        W = self.W
+        W.name, W.schema = "config5-quota", QUOTA_SCHEMA
+        W.ids = corc.Ids(ref.Schema(QUOTA_SCHEMA))
+        self.limits = np.sort(self.rng.choice(1 << 20, n_limits, replace=False)).astype(np.int64)
+        # per caveated relationship: the index of its limit
+        self.lim = {k: self.rng.integers(0, n_limits, int(c.sum())) for k, (_, c) in self.state.items()}
+
+    def load(self, eng, plain_csr_loader, cav_instance=None):
+        """Static and plain CSRs through `plain_csr_loader`; one caveat instance per distinct
+        limit (gck_add_caveat_instance) and the caveated relationships as interned tuples."""
+        from gochugaru_amd.engine import TUPLE_DTYPE
+        self.inst = np.array([eng.add_caveat_instance("quota", '{"limit":%d}' % v) for v in self.limits],
+                             dtype=np.uint32)
+        for c in self.static:
+            plain_csr_loader(*c)
+        tups = []
+        for (rid, st, sr), (keys, cav) in self.state.items():
+            n_rows = self.W.counts[self.W.ids.rels[rid][0]]
+            off, nbr = self._csr(keys[~cav], n_rows)
+            plain_csr_loader(rid, st, sr, n_rows, torch.from_numpy(off.astype(np.int64)).to(self.device),
+                             torch.from_numpy(nbr.view(np.int32)).to(self.device))
+            t = np.zeros(int(cav.sum()), dtype=TUPLE_DTYPE)
+            t["resource_type"] = self.W.t(self.W.ids.rels[rid][0])
+            t["relation"] = rid
+            t["resource_id"] = keys[cav] >> np.uint64(32)
+            t["subject_type"] = st
+            t["subject_relation"] = sr
+            t["subject_id"] = keys[cav] & np.uint64(0xFFFFFFFF)
+            t["caveat"] = self.inst[self.lim[(rid, st, sr)]]
+            tups.append(t)
+        eng.add_tuples(np.concatenate(tups))
+
+    def checks(self, n: int, seed: int, bad: float = 0.0):
+        """(items [n, 20] u8 on the device, used values i64[n_slots], context texts): check i
+        has context slot i + 1 with its own `used` (10 % have slot 0: no context); a fraction
+        `bad` of the contexts give `used` a string (an evaluation error when a walk meets it)."""
+        items = checks(self.W, n, seed)
+        rng = np.random.default_rng(seed + 7)
+        used = rng.integers(0, 1 << 20, n).astype(np.int64)
+        texts = ['{"used":%d}' % u for u in used]
+        for i in np.nonzero(rng.random(n) < bad)[0]:
+            used[i] = BAD_USED
+            texts[i] = '{"used":"many"}'
+        slot = np.arange(1, n + 1, dtype=np.int64)
+        slot[rng.random(n) < 0.1] = 0
+        items.view(torch.int32).reshape(n, 5)[:, 4] = torch.from_numpy(slot.astype(np.int32)).to(items.device)
+        return items, used, texts
+
+    def expected(self, items_host: np.ndarray, used: np.ndarray, threads: int = 16):
+        """(perm, err) from the C oracle's threshold mode over the same snapshot."""
+        prog, tab, limits = self.oracle()
+        return corc.check_quota(prog, tab, items_host, limits, used, threads=threads)
+
+    def oracle(self):
+        """(program, csr table, limit per caveat id) for corc.check_quota."""
+        idx, arrays = {}, []
+        for rid, st, sr, n_rows, off, nbr in self.static:
+            idx[(rid, st, sr, False)] = len(arrays)
+            arrays.append((off.to(torch.int64).cpu().numpy().astype(np.uint32),
+                           nbr.cpu().numpy().view(np.uint32), None, None, n_rows))
+        for (rid, st, sr), (keys, cav) in self.state.items():
+            n_rows = self.W.counts[self.W.ids.rels[rid][0]]
+            off, nbr = self._csr(keys[~cav], n_rows)
+            idx[(rid, st, sr, False)] = len(arrays)
+            arrays.append((off, nbr, None, None, n_rows))
+            if cav.any():
+                off, nbr = self._csr(keys[cav], n_rows)  # keys are sorted: rows in order
+                idx[(rid, st, sr, True)] = len(arrays)
+                cid = (self.lim[(rid, st, sr)] + 1).astype(np.uint32)
+                arrays.append((off, nbr, cid, np.zeros(nbr.size, np.int64), n_rows))
+        prog = corc.encode_program(self.W.ids, idx)
+        return prog, corc.make_csr_table(arrays), np.concatenate([[0], self.limits]).astype(np.int64)

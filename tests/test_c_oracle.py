@@ -62,3 +62,88 @@ def test_count_bfs_rule():
     st = corc.Store(ref.Schema(schema), [ref.parse_tuple(t) for t in tuples])
     with pytest.raises(ValueError):
         corc.count_bfs(st.program, st.csr_table(), st.items([to_oracle_item(parse_check(checks[0]))]))
+
+
+QUOTA = """
+caveat quota(limit int, used int) {
+  used < limit
+}
+definition user {}
+definition group {
+  relation member: user | user with quota | group#member
+}
+definition doc {
+  relation viewer: user | user with quota | group#member | group#member with quota
+  relation banned: user with quota
+  permission view = viewer - banned
+}
+"""
+
+
+def quota_case(seed, n_checks=300):
+    import random
+    rng = random.Random(seed)
+    users = [f"u{i}" for i in range(25)]
+    tuples = []
+    for g in range(6):
+        for u in rng.sample(users, 4):
+            tuples.append(f"group:g{g}#member@user:{u}" + (f'[quota:{{"limit":{rng.randrange(100)}}}]'
+                                                            if rng.random() < 0.5 else ""))
+        if g < 5 and rng.random() < 0.6:
+            tuples.append(f"group:g{g}#member@group:g{rng.randrange(g + 1, 6)}#member")
+    for d in range(15):
+        for u in rng.sample(users, 3):
+            tuples.append(f"doc:d{d}#viewer@user:{u}" + (f'[quota:{{"limit":{rng.randrange(100)}}}]'
+                                                          if rng.random() < 0.6 else ""))
+        g = rng.randrange(6)
+        tuples.append(f"doc:d{d}#viewer@group:g{g}#member" + (f'[quota:{{"limit":{rng.randrange(100)}}}]'
+                                                              if rng.random() < 0.5 else ""))
+        if rng.random() < 0.4:
+            tuples.append(f'doc:d{d}#banned@user:{rng.choice(users)}[quota:{{"limit":{rng.randrange(100)}}}]')
+    checks = [f"doc:d{rng.randrange(15)}#view@user:{rng.choice(users)}" for _ in range(n_checks)]
+    used = [None if rng.random() < 0.15 else rng.randrange(100) for _ in checks]
+    return tuples, checks, used
+
+
+def run_quota(tuples, checks, used, threads=1):
+    """(Python oracle, C oracle threshold mode) answers of the checks; used[i] None = no context,
+    a string = a wrongly typed `used`."""
+    sc = ref.Schema(QUOTA)
+    tps = [ref.parse_tuple(t) for t in tuples]
+    py = ref.Checker(sc, ref.TupleStore(tps))
+    items = [to_oracle_item(parse_check(c), None if u is None else {"used": u}) for c, u in zip(checks, used)]
+    want = [py.check(it) for it in items]
+    st = corc.Store(sc, tps)
+    limits = [0] + [dict(ctx)["limit"] for _, ctx in st.caveats[1:]]
+    ci = st.items(items)
+    vals = []
+    for i, u in enumerate(used):
+        if u is not None:
+            vals.append(corc_used(u))
+            ci[i]["context_slot"] = len(vals)
+    perm, err = corc.check_quota(st.program, st.csr_table(), ci, np.array(limits), np.array(vals, dtype=np.int64),
+                                 threads=threads)
+    return want, [(int(p), int(e)) for p, e in zip(perm, err)]
+
+
+def corc_used(u):
+    return np.iinfo(np.int64).min if isinstance(u, str) else u
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_c_oracle_quota_mode_matches_python_oracle(seed):
+    tuples, checks, used = quota_case(seed)
+    want, got = run_quota(tuples, checks, used, threads=2)
+    bad = [(c, u, w, g) for c, u, w, g in zip(checks, used, want, got) if w != g]
+    assert not bad, bad[:10]
+    assert {w[0] for w in want} >= {1, 2, 3}
+
+
+def test_caveat_eval_error_fails_only_its_checks():
+    """A wrongly typed `used` is an error for the checks whose walk meets the caveat, and for no
+    other (single-path data: the walk order cannot matter)."""
+    tuples = ['doc:a#viewer@user:x[quota:{"limit":10}]', "doc:b#viewer@user:x", "doc:c#viewer@user:y"]
+    checks = ["doc:a#view@user:x", "doc:b#view@user:x", "doc:c#view@user:x", "doc:a#view@user:x"]
+    used = ["many", "many", "many", 3]
+    want, got = run_quota(tuples, checks, used)
+    assert want == got == [(0, ref.ITEM_ERR_CAVEAT_EVAL), (ref.HAS, 0), (ref.NO, 0), (ref.HAS, 0)]
