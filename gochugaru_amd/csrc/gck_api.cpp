@@ -519,6 +519,44 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
   });
 }
 
+// What a text Watch batch may add before it is known to apply: new interned ids (CREATE of an
+// unseen object) and new caveat instances. A rejected batch takes them back, so that nothing of
+// it stays (interner counts are also the CSR row counts of the next batch).
+struct InternMark {
+  std::vector<uint32_t> counts;
+  size_t n_cav = 0, n_partial = 0;
+};
+
+static InternMark intern_mark(const Engine& e) {
+  InternMark m;
+  for (const TypeInterner& ti : e.interner) m.counts.push_back(ti.count);
+  m.n_cav = e.caveat_instances.size();
+  m.n_partial = e.caveat_partial.size();
+  return m;
+}
+
+static void intern_rollback(Engine& e, const InternMark& m) {
+  for (size_t t = 0; t < m.counts.size() && t < e.interner.size(); ++t) {
+    TypeInterner& ti = e.interner[t];
+    for (uint32_t id = m.counts[t]; id < ti.names.size(); ++id)
+      if (!ti.names[id].empty()) ti.ids.erase(ti.names[id]);
+    if (ti.names.size() > m.counts[t]) ti.names.resize(m.counts[t]);
+    ti.count = m.counts[t];
+  }
+  for (size_t id = m.n_cav; id < e.caveat_instances.size(); ++id) {
+    std::string key = e.caveat_instances[id].first;  // add_caveat_instance's key
+    key += '\0';
+    key += e.caveat_instances[id].second;
+    e.caveat_ids.erase(key);
+  }
+  e.caveat_instances.resize(m.n_cav);
+  e.caveat_expr.resize(m.n_cav);
+  e.caveat_ctx.resize(m.n_cav);
+  e.caveat_static.resize(m.n_cav);
+  e.caveat_row.resize(m.n_cav);
+  e.caveat_partial.resize(m.n_partial);
+}
+
 int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, size_t len) {
   return guard([&] {
     Engine& e = need(ge);
@@ -526,10 +564,20 @@ int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, 
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
     std::unique_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    // the revision first: a stale batch is refused before its text is read
+    REQUIRE(revision > e.revision || (len == 0 && revision == e.revision), GCK_E_REVISION,
+            "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
+                std::to_string(e.revision));
     drain_batches(e);
-    std::vector<gck_update> ups;
-    parse_updates_text(e, text, len, ups);
-    apply_updates(e, revision, ups);
+    const InternMark mark = intern_mark(e);
+    try {
+      std::vector<gck_update> ups;
+      parse_updates_text(e, text, len, ups);
+      apply_updates(e, revision, ups);
+    } catch (...) {
+      intern_rollback(e, mark);
+      throw;
+    }
   });
 }
 

@@ -119,6 +119,7 @@ void save_snapshot_file(Engine& e, const std::string& path) {
 void load_snapshot_file(Engine& e, const std::string& path) {
   if (!e.schema) throw Error(GCK_E_STATE, "gck_load_schema first");
   if (e.staging) throw Error(GCK_E_STATE, "a snapshot is being staged");
+  if (e.part_world > 1) throw Error(GCK_E_STATE, "a partitioned engine holds only its rank's rows");
   File f(path, "rb");
   char magic[8];
   f.get(magic, sizeof(magic));
@@ -165,17 +166,34 @@ void load_snapshot_file(Engine& e, const std::string& path) {
     (void)f.get_v<uint8_t>();
     h.n_rows = f.get_v<uint32_t>();
     const uint64_t ne = f.get_v<uint64_t>();
-    bool allowed = h.rel < sc.rels.size() && !sc.rels[h.rel].is_perm;
-    if (allowed) {
-      allowed = false;
-      for (const Allowed& a : sc.rels[h.rel].allowed) allowed |= a.stype == h.stype && a.srel == h.srel;
+    // the kind must be one the schema allows, with one row per object of the relation's type and
+    // neighbours that are objects of the subject type (or the wildcard, where allowed), each row
+    // strictly ascending: what build_csrs produces and device_upload's kernels index by
+    bool allowed = false, wildcard = false;
+    if (h.rel < sc.rels.size() && !sc.rels[h.rel].is_perm) {
+      for (const Allowed& a : sc.rels[h.rel].allowed) {
+        allowed |= a.stype == h.stype && a.srel == h.srel;
+        wildcard |= a.wildcard && a.stype == h.stype && h.srel == kEllipsis;
+      }
     }
-    if (!allowed || ne >= 0xFFFFFFFFull) throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (CSR)");
+    if (!allowed || ne >= 0xFFFFFFFFull || h.stype >= n_types)
+      throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (CSR)");
+    if (h.n_rows != interner[sc.rels[h.rel].type].count)
+      throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (CSR rows differ from the object count)");
     h.off.resize((size_t)h.n_rows + 1);
     f.get(h.off.data(), h.off.size() * 4);
     if (h.off[0] != 0 || h.off.back() != ne) throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (offsets)");
+    for (uint32_t r = 0; r < h.n_rows; ++r)
+      if (h.off[r] > h.off[r + 1]) throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (offsets)");
     h.nbr.resize(ne);
     f.get(h.nbr.data(), ne * 4);
+    const uint32_t n_subjects = interner[h.stype].count;
+    for (uint32_t r = 0; r < h.n_rows; ++r)
+      for (uint32_t k = h.off[r]; k < h.off[r + 1]; ++k) {
+        const uint32_t v = h.nbr[k];
+        if (!(v < n_subjects || (v == GCK_ID_WILDCARD && wildcard)) || (k > h.off[r] && h.nbr[k - 1] >= v))
+          throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (neighbours)");
+      }
     if (h.ext) {
       h.cav.resize(ne);
       h.exp_us.resize(ne);
@@ -188,16 +206,35 @@ void load_snapshot_file(Engine& e, const std::string& path) {
   }
   if (f.get_v<uint64_t>() != kEnd) throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (end marker)");
   if (total != n_tuples) throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (tuple count)");
-  // install: caveat instances keep their ids (the CSRs refer to them), then the device upload
-  e.committed = false;
-  reset_caveats(e);
-  for (uint32_t k = 0; k < n_cav; ++k)
-    if (add_caveat_instance(e, cavs[k].first, cavs[k].second) != k + 1)
-      throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (duplicate caveat instance)");
-  e.interner = std::move(interner);
+  // install: caveat instances keep their ids (the CSRs refer to them), then the device upload;
+  // on any failure the engine keeps its previous interner, caveat tables and device snapshot
+  auto cav_instances = e.caveat_instances;
+  auto cav_ids = e.caveat_ids;
+  auto cav_expr = e.caveat_expr;
+  auto cav_ctx = e.caveat_ctx;
+  auto cav_static = e.caveat_static;
+  auto cav_row = e.caveat_row;
+  auto cav_partial = e.caveat_partial;
+  std::swap(e.interner, interner);
+  try {
+    reset_caveats(e);
+    for (uint32_t k = 0; k < n_cav; ++k)
+      if (add_caveat_instance(e, cavs[k].first, cavs[k].second) != k + 1)
+        throw Error(GCK_E_INVALID_ARGUMENT, "corrupt snapshot file (duplicate caveat instance)");
+    device_upload(e, csrs);
+  } catch (...) {
+    std::swap(e.interner, interner);
+    e.caveat_instances = std::move(cav_instances);
+    e.caveat_ids = std::move(cav_ids);
+    e.caveat_expr = std::move(cav_expr);
+    e.caveat_ctx = std::move(cav_ctx);
+    e.caveat_static = std::move(cav_static);
+    e.caveat_row = std::move(cav_row);
+    e.caveat_partial = std::move(cav_partial);
+    throw;
+  }
   e.prebuilt.clear();
   e.staged.clear();
-  device_upload(e, csrs);
   e.n_tuples = n_tuples;
   e.revision = revision;
   e.committed = true;

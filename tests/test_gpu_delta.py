@@ -157,6 +157,16 @@ def test_client_apply_updates_and_consistency():
     assert ei.value.code == E.GCK_E_INVALID_ARGUMENT
     with pytest.raises(E.GckError):
         e.apply_updates_text(6, "UPSERT company:authzed#founder@user:jake")
+    # a rejected batch leaves no interned ids behind (a new user and company in its valid lines)
+    user, company = e.type_id("user"), e.type_id("company")
+    n_users, n_companies = e.object_count(user), e.object_count(company)
+    with pytest.raises(E.GckError):
+        e.apply_updates_text(6, "CREATE company:newco#founder@user:newbie\nCREATE company:newco#nosuch@user:x")
+    with pytest.raises(E.GckError) as ei:  # stale: refused before the text is read
+        e.apply_updates_text(5, "CREATE company:other#founder@user:someone")
+    assert ei.value.code == E.GCK_E_REVISION
+    assert (e.object_count(user), e.object_count(company)) == (n_users, n_companies)
+    assert e.intern(user, ["newbie", "someone"]).tolist() == [E.ID_ABSENT, E.ID_ABSENT]
     assert e.revision == 5
     assert c.Check(None, consistency.Full(), *founders) == ([False, True, True], None)
     # an empty batch may advance the revision (a Watch checkpoint)

@@ -155,6 +155,46 @@ def test_rejects_foreign_and_corrupt_files(tmp_path):
     e.close()
 
 
+def _snapfile(schema, counts, rows, off, nbr, n_tuples=None):
+    """A hand-written snapshot file (snapfile.cpp layout) with one plain CSR of relation 0."""
+    le = lambda v, n: int(v).to_bytes(n, "little")
+    b = b"GCKSNAP\x01" + le(len(schema), 8) + schema.encode() + le(7, 8) + le(len(nbr) if n_tuples is None else n_tuples, 8)
+    b += le(len(counts), 4) + b"".join(le(c, 4) + le(0, 4) for c in counts)
+    b += le(0, 4) + le(1, 4)
+    b += le(0, 2) + le(0, 2) + le(0xFFFF, 2) + le(0, 1) + le(0, 1) + le(rows, 4) + le(len(nbr), 8)
+    b += np.asarray(off, np.uint32).tobytes() + np.asarray(nbr, np.uint32).tobytes()
+    return b + le(0x444E455041534B43, 8)
+
+
+@pytest.mark.parametrize("case", ["rows", "offsets", "neighbour", "unsorted", "wildcard"])
+def test_rejects_inconsistent_csrs(tmp_path, case):
+    """A file whose CSR disagrees with its own interner (row count, neighbour ids), or whose
+    offsets / rows are not what build_csrs writes, is refused before any device upload, and the
+    engine keeps its state."""
+    schema = "definition user {}\ndefinition company { relation founder: user }"
+    counts = [4, 3]  # users, companies
+    off, nbr, rows = [0, 1, 3, 4], [2, 0, 3, 1], 3
+    if case == "rows":
+        rows, off = 2, [0, 1, 4]
+    elif case == "offsets":
+        off = [0, 3, 1, 4]
+    elif case == "neighbour":
+        nbr = [2, 0, 4, 1]
+    elif case == "unsorted":
+        nbr = [2, 3, 0, 1]
+    elif case == "wildcard":
+        nbr = [2, 0, 0xFFFFFFFF, 1]
+    path = tmp_path / f"{case}.gck"
+    path.write_bytes(_snapfile(schema, counts, rows, off, nbr))
+    e = E.Engine()
+    e.load_schema(schema)
+    with pytest.raises(E.GckError) as ei:
+        e.load_snapshot_file(str(path))
+    assert ei.value.code == E.GCK_E_INVALID_ARGUMENT, ei.value
+    assert e.revision == 0
+    e.close()
+
+
 @pytest.mark.gpu
 def test_interned_pages_match_text_ingest():
     """gck_add_tuples pages (threaded validation + radix-sorted CSR build) give the snapshot the
