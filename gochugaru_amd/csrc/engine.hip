@@ -20,6 +20,7 @@
 // Every frontier level is one dispatch wave of SpiceDB's recursion, so the depth budget
 // (max_depth, default 50) is enforced per entry exactly as dispatch.CheckDepth does.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1195,6 +1196,7 @@ static void free_workspace(Workspace* w) {
 }
 
 void device_free(Engine& e) {
+  part_comm_free(e);
   if (e.delta_scratch) {
     (void)hipSetDevice(e.device);
     (void)hipFree(e.delta_scratch);
@@ -2541,6 +2543,7 @@ static PartState& part_state(Workspace& w) {
 
 static void free_part(PartState* p) {
   if (!p) return;
+  free_xfer(p->xfer);
   if (p->h_out) (void)hipHostFree(p->h_out);
   delete p;  // outbox / out_cnt are in the workspace's allocation list
 }

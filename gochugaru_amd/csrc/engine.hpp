@@ -188,6 +188,7 @@ struct Engine {
   std::vector<Workspace*> ws_pool;
   Workspace* part_ws = nullptr;   // the partitioned batch's own workspace (partition.inc)
   uint64_t part_generation = 0;   // the snapshot generation a partitioned batch started on
+  void* part_comm = nullptr;      // ncclComm_t of gck_part_init (partition.inc)
   std::mutex stats_mu;            // stats are added by concurrent batches
   std::mutex host_mu;             // pinned host buffers handed out by gck_host_alloc (base -> bytes)
   std::map<uintptr_t, size_t> host_bufs;
@@ -265,6 +266,11 @@ void part_pack(Engine& e, void* d_send, size_t send_cap);
 void part_ingest(Engine& e, const void* d_recv, size_t n_recv, void* d_flags);
 uint32_t part_resolve(Engine& e, const void* d_flags);
 void part_finish(Engine& e, uint8_t* d_perm, int32_t* d_err);
+void part_unique_id(uint8_t* out);
+void part_init(Engine& e, const uint8_t* id);
+void part_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm, int32_t* d_err,
+                void* stream);
+void part_comm_free(Engine& e);
 void device_free(Engine& e);
 
 }  // namespace gck

@@ -837,6 +837,33 @@ int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
   });
 }
 
+int gck_part_unique_id(uint8_t* out) {
+  return guard([&] {
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null id buffer");
+    part_unique_id(out);
+  });
+}
+
+int gck_part_init(gck_engine* ge, const uint8_t* id) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(id, GCK_E_INVALID_ARGUMENT, "null id");
+    std::unique_lock<std::shared_mutex> lk(e.mu);
+    part_init(e, id);
+  });
+}
+
+int gck_part_check(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_out_perm,
+                   int32_t* d_out_err, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    part_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream);
+  });
+}
+
 // The result of a lookup that did not fit the caller's buffer, kept per thread so that the retry
 // with cap >= *out_n copies it out without a second sweep. It matches only a retry of the same
 // request on the same snapshot (process-wide snapshot generation) at the same explicit now_us

@@ -188,6 +188,9 @@ _SIGS = {
     "gck_part_ingest": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "gck_part_resolve": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "gck_part_finish": (C.c_int, [_P, _P, _P]),
+    "gck_part_unique_id": (C.c_int, [_P]),
+    "gck_part_init": (C.c_int, [_P, _P]),
+    "gck_part_check": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_reset_stats": (C.c_int, [_P]),
 }
 
@@ -564,6 +567,24 @@ class Engine:
     def part_finish(self, d_perm: int, d_err: int):
         _check(self._lib.gck_part_finish(self._h, d_perm, d_err))
 
+    @staticmethod
+    def part_unique_id() -> bytes:
+        """gck_part_unique_id: the RCCL communicator id rank 0 hands to every rank."""
+        buf = (C.c_uint8 * PART_UNIQUE_ID_BYTES)()
+        _check(load_library().gck_part_unique_id(buf))
+        return bytes(buf)
+
+    def part_init(self, unique_id: bytes):
+        """gck_part_init: join the RCCL communicator of the partition (every rank, same id)."""
+        assert len(unique_id) == PART_UNIQUE_ID_BYTES
+        buf = (C.c_uint8 * PART_UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        _check(self._lib.gck_part_init(self._h, buf))
+
+    def part_check(self, d_items: int, n: int, d_perm: int, d_err: int, now_us: int = 0,
+                   stream: Optional[int] = None):
+        """gck_part_check: the whole partitioned check, exchanged over RCCL inside libgck."""
+        _check(self._lib.gck_part_check(self._h, d_items, n, now_us, d_perm, d_err, stream))
+
     def stats(self) -> Stats:
         s = _Stats()
         _check(self._lib.gck_last_stats(self._h, C.byref(s)))
@@ -676,6 +697,7 @@ def _context_arrays(contexts):
 
 
 PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES
+PART_UNIQUE_ID_BYTES = 128  # GCK_PART_UNIQUE_ID_BYTES
 
 
 def part_flag_bytes(n: int) -> int:

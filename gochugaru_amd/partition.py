@@ -102,3 +102,34 @@ class PartitionedChecker:
                 break
         eng.part_finish(perm.data_ptr(), err.data_ptr())
         return perm, err
+
+
+class RcclPartitionedChecker:
+    """Checks global batches on a partitioned engine with the level loop and its exchange inside
+    libgck (``gck_part_check``: grouped RCCL send / receive + all-reduce over xGMI, one process
+    per GPU). ``group`` (any torch.distributed backend) only carries the communicator id from
+    rank 0 to the others, once."""
+
+    def __init__(self, engine: Engine, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.engine = engine
+        self.torch = torch
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        assert engine.part_world == world and engine.part_rank == rank, \
+            "engine partition (set_partition) must match the process group"
+        box = [Engine.part_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(box, src=0, group=group)
+        engine.part_init(box[0])
+
+    def check(self, d_items, n: int, now_us: int = 0):
+        torch = self.torch
+        perm = torch.zeros(n, dtype=torch.uint8, device=d_items.device)
+        err = torch.zeros(n, dtype=torch.int32, device=d_items.device)
+        stream = torch.cuda.current_stream(d_items.device).cuda_stream
+        self.engine.part_check(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us, stream)
+        return perm, err
+

@@ -372,7 +372,8 @@ int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resou
  *     gck_part_resolve(flags, &active)              identical `active` on every rank; 0 = done
  *   gck_part_finish(perm, err)                      every rank gets every result
  *
- * The caller owns the exchange (RCCL all_to_all / all_reduce over xGMI, or any transport).
+ * The caller owns the exchange (RCCL all_to_all / all_reduce over xGMI, or any transport), or
+ * gck_part_check runs the loop with RCCL inside libgck (below).
  * Union schemas only (no &, -, all()); check-time caveat contexts are not taken. A partitioned
  * engine refuses gck_check_bulk*. */
 #define GCK_PART_ENTRY_BYTES 12
@@ -386,6 +387,21 @@ int gck_part_pack(gck_engine* e, void* d_send, size_t send_cap);
 int gck_part_ingest(gck_engine* e, const void* d_recv, size_t n_recv, void* d_flags);
 int gck_part_resolve(gck_engine* e, const void* d_flags, uint32_t* out_active);
 int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
+
+/* The whole partitioned check inside libgck, exchanging over RCCL (xGMI between the GPUs of a
+ * node): the loop above with grouped ncclSend / ncclRecv for the counts and the entries and an
+ * in-place ncclAllReduce(MAX) of the flag bytes, no host round trip through the caller per
+ * level. Rank 0 makes the id (gck_part_unique_id), the caller hands the same bytes to every rank
+ * (any transport: a TCP store, MPI, a file), and each rank — one process per GPU, the engine's
+ * device — joins with gck_part_init after gck_set_partition. gck_part_check then takes the place
+ * of the begin .. finish sequence; every rank calls it with the same items and gets every
+ * result. `stream` orders the batch after the caller's writes of the items (NULL: the legacy
+ * default stream). */
+#define GCK_PART_UNIQUE_ID_BYTES 128
+int gck_part_unique_id(uint8_t out[GCK_PART_UNIQUE_ID_BYTES]);
+int gck_part_init(gck_engine* e, const uint8_t id[GCK_PART_UNIQUE_ID_BYTES]);
+int gck_part_check(gck_engine* e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_out_perm,
+                   int32_t* d_out_err, void* stream);
 
 #ifdef __cplusplus
 }

@@ -121,3 +121,29 @@ def test_partitioned_rejects_joins():
         e.part_begin(d.data_ptr(), 1)
     assert ei.value.code == E.GCK_E_INVALID_ARGUMENT
     e.close()
+
+
+@pytest.mark.parametrize("family,seed", [("nested", 1), ("gdocs", 2), ("gdocs_deep", 3)])
+def test_rccl_loop_single_rank_matches_oracle(family, seed):
+    """gck_part_check: the level loop with its RCCL exchange inside libgck (grouped send / receive
+    of counts and entries, in-place all-reduce MAX of the flags). The one-GPU test box can only
+    hold a one-rank communicator (RCCL refuses two ranks on one GPU: "Duplicate GPU detected"),
+    so this runs the whole RCCL path with world 1; the multi-rank exchange protocol itself is
+    covered by the gloo tests above and tests/test_partition_cpu.py."""
+    from gochugaru_amd.partition import RcclPartitionedChecker
+    schema, tuples, checks = gen.FAMILIES[family](seed)
+    e = E.Engine(device=0)
+    e.load_schema(schema)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    items = e.make_items([parse_check(c) for c in checks])
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    pc = RcclPartitionedChecker(e)
+    perm, err = pc.check(d_items, len(items), now_us=gen.NOW_US)
+    got = list(zip(perm.cpu().tolist(), err.cpu().tolist()))
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+    bad = [(c, w, g) for c, w, g in zip(checks, want, got) if tuple(w) != tuple(g)]
+    assert not bad, bad[:5]
+    perm2, err2 = pc.check(d_items, len(items), now_us=gen.NOW_US)  # the communicator is reused
+    assert perm2.cpu().tolist() == perm.cpu().tolist() and err2.cpu().tolist() == err.cpu().tolist()
+    e.close()
