@@ -550,7 +550,9 @@ def main():
                        "bundle_ms_per_batch": round(st["bundle_ms"] / n_batches, 4),
                        "deferred_per_batch": round(st["deferred"] / n_batches, 1),
                        "giant_ms_per_batch": round(st["giant_ms"] / n_batches, 4),
-                       "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2)},
+                       "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2),
+                       "closure_checks_per_batch": round(st["closure_checks"] / n_batches, 1),
+                       "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
             **({"caveats": {"evals_per_step": round(st["caveat_evals"] / args.steps, 1),
                             "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}

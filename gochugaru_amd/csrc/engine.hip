@@ -61,6 +61,8 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
   uint64_t src_edges;
   DevCSR d;
   uint32_t* sig = nullptr;  // ancestor closure: 256-bit signature per row (closure.inc)
+  uint32_t* sig512 = nullptr;  // ... 512-bit signature per row (the slot fast path's user signatures)
+  uint32_t* lab = nullptr;     // ... tree labels per row: {pre | impure << 31, end} (closure.inc)
 };
 
 struct DeviceSnapshot {
@@ -1694,6 +1696,7 @@ static void add_counters(Engine& e, Workspace& w, const DevCounters& h) {
   e.stats.levels += h.bundle_levels;
   e.stats.bundles += h.bundles;
   e.stats.closure_checks += h.closure;
+  e.stats.slot_checks += h.slot_checks;
 }
 
 // Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
@@ -1862,7 +1865,8 @@ static BundleArgs bundle_args(Engine& e, Workspace& w, const gck_item* d_items, 
   a.n_dev = nullptr;
   // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
-  const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
+  // bundle records of stages A and B, then the closure join's per-wave records
+  const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2 + (size_t)kCjTimingWords * (n / 64 + 1);
   if (timing_env && w.timing_cap < timing_words) {
     if (w.timing) (void)hipFree(w.timing);
     w.timing = nullptr;
@@ -1931,6 +1935,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.table_bytes = (uint32_t)((ds.cj_host.size() + 3) & ~(size_t)3);
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
+    j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
     hipLaunchKernelGGL(k_closure_join, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
     HIP_OK(hipGetLastError());
   } else {
@@ -2092,14 +2097,24 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
   }
   if (timing_env && w.timing) {
     const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
-    std::vector<unsigned long long> h(timing_words);
-    HIP_OK(hipMemcpy(h.data(), w.timing, timing_words * 8, hipMemcpyDeviceToHost));
+    const size_t cj_words = (size_t)kCjTimingWords * (n / 64 + 1);
+    std::vector<unsigned long long> h(timing_words + cj_words);
+    HIP_OK(hipMemcpy(h.data(), w.timing, (timing_words + cj_words) * 8, hipMemcpyDeviceToHost));
     std::string path = std::string(timing_env) + ".bin";
     if (FILE* f = fopen(path.c_str(), "ab")) {
       unsigned long long hdr[4] = {0xB0DDull, n, w.b_checks, w.h_bctrs[1]};
       fwrite(hdr, 8, 4, f);
       fwrite(h.data(), 8, timing_words, f);
       fclose(f);
+    }
+    if (w.b_closure) {  // the closure join's per-wave records: <prefix>_cj.bin
+      std::string cpath = std::string(timing_env) + "_cj.bin";
+      if (FILE* f = fopen(cpath.c_str(), "ab")) {
+        unsigned long long hdr[2] = {0xC10Cull, (n + 63) / 64};
+        fwrite(hdr, 8, 2, f);
+        fwrite(h.data() + timing_words, 8, (size_t)kCjTimingWords * ((n + 63) / 64), f);
+        fclose(f);
+      }
     }
   }
   (void)e;

@@ -193,6 +193,7 @@ struct DevCounters {  // device-side counters, reset per level where noted
   unsigned long long bundle_levels; // BFS levels run by bundles (summed over bundles)
   unsigned long long bundles;       // bundles run
   unsigned long long closure;       // checks answered by the closure-join stage (closure.inc)
+  unsigned long long slot_checks;   // checks the closure join's slot test decided (closure.inc)
   unsigned int cav_requests;        // (caveat instance, check context) pairs recorded for evaluation
   unsigned int cav_errors;          // touched pairs whose evaluation failed
 };

@@ -57,6 +57,7 @@ FLAG_NO_GIANT = 8
 FLAG_NO_BIDIR = 16
 FLAG_NO_CLOSURE = 32
 FLAG_LAZY_CAVEATS = 64
+FLAG_NO_SLOTS = 128
 SUBMIT_DEVICE = 1
 
 ITEM_DTYPE = np.dtype([
@@ -122,7 +123,7 @@ class _Stats(C.Structure):
                 ("bundle_launches", C.c_uint64), ("deferred", C.c_uint64),
                 ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64),
                 ("bidir_checks", C.c_uint64), ("bundles", C.c_uint64), ("closure_checks", C.c_uint64),
-                ("caveat_evals", C.c_uint64), ("caveat_passes", C.c_uint64)]
+                ("caveat_evals", C.c_uint64), ("caveat_passes", C.c_uint64), ("slot_checks", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
@@ -244,12 +245,12 @@ class Engine:
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
                  giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
                  bidir: bool = True, bidir_both: int = 0, workspaces: int = 0, closure: bool = True,
-                 lazy_caveats: bool = False):
+                 lazy_caveats: bool = False, slots: bool = True):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
                  | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
                  | (0 if bidir else FLAG_NO_BIDIR) | (0 if closure else FLAG_NO_CLOSURE)
-                 | (FLAG_LAZY_CAVEATS if lazy_caveats else 0))
+                 | (FLAG_LAZY_CAVEATS if lazy_caveats else 0) | (0 if slots else FLAG_NO_SLOTS))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,

@@ -110,6 +110,8 @@ extern "C" {
 #define GCK_FLAG_NO_BIDIR 16u    /* gck_config.flags: forward-only search (no bidirectional checks) */
 #define GCK_FLAG_NO_CLOSURE 32u  /* gck_config.flags: no closure-join stage (nested-group checks take
                                     the bundle search) */
+#define GCK_FLAG_NO_SLOTS 128u  /* gck_config.flags: no per-user / per-resource slots for the
+                                   closure join (saves ~128 B per user of HBM; slower) */
 #define GCK_FLAG_LAZY_CAVEATS 64u /* gck_config.flags: always evaluate check-time caveat contexts
                                      lazily (only the pairs a walk meets; by default a call whose
                                      partial instances x distinct contexts is small evaluates them all) */
@@ -210,6 +212,8 @@ typedef struct gck_stats {
   uint64_t closure_checks;     /* checks answered by the closure-join stage (nested groups) */
   uint64_t caveat_evals;       /* (caveat instance, check context) pairs evaluated on the host */
   uint64_t caveat_passes;      /* extra batch passes after lazily evaluated caveat pairs */
+  uint64_t slot_checks;        /* checks the closure join decided from their user / resource slots
+                                  alone (one read each) */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

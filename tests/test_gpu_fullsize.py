@@ -48,6 +48,7 @@ def test_config4_1e9_full_batch():
     assert n_bad == 0, first
     assert np.array_equal(gp2, gp) and np.array_equal(ge2, ge)
     assert st["closure_checks"] == N  # every check answered by the closure join
+    assert st["slot_checks"] > N // 2  # most from the user / resource slots alone
     assert 0.3 < np.mean(cp == 2) < 0.7
 
 

@@ -183,6 +183,8 @@ PATHS = {
     "giant-skip": {"bundle_budget": 2, "giant_stage": False, "closure": False},
     # what the closure-join stage leaves goes through the bundles' deferral chain
     "closure-giant": {"bundle_budget": 2},
+    # the closure join's task rounds alone (no user / resource slots)
+    "noslots": {"slots": False},
     # one check per wavefront, few resident waves
     "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4, "closure": False},
     # binary-search membership instead of the hashed index, both paths
@@ -218,6 +220,10 @@ def test_random_parity(family, seed, path):
         assert e.stats()["deferred"] == 0
     if path == "bundle" and family in ("nested", "gdocs_deep"):
         assert e.stats()["closure_checks"] > 0  # nested doc#view / group#member checks
+    if path == "bundle" and family == "nested":
+        assert e.stats()["slot_checks"] > 0  # doc#view@user decided from the slots
+    if path == "noslots":
+        assert e.stats()["slot_checks"] == 0
     if path == "noclosure" and family in ("nested", "gdocs_deep"):
         assert e.stats()["bidir_checks"] > 0 and e.stats()["closure_checks"] == 0
     if path in ("nobidir", "wide") or family == "caveated":
