@@ -61,8 +61,9 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
   uint64_t src_edges;
   DevCSR d;
   uint32_t* sig = nullptr;  // ancestor closure: 256-bit signature per row (closure.inc)
-  uint32_t* sig512 = nullptr;  // ... 512-bit signature per row (the slot fast path's user signatures)
-  uint32_t* lab = nullptr;     // ... tree labels per row: {pre | impure << 31, end} (closure.inc)
+  uint32_t* lab = nullptr;      // ... tree labels per row: {pre | cover overflow << 31, end} (closure.inc)
+  uint32_t* cov_off = nullptr;  // ... tree cover per row (preorder numbers), CSR
+  uint32_t* cov_pre = nullptr;
 };
 
 struct DeviceSnapshot {
