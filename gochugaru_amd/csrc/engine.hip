@@ -68,6 +68,7 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
 
 struct DeviceSnapshot {
   std::vector<void*> allocs;
+  std::vector<void*> hallocs;  // hipExtMallocWithFlags (physically contiguous) arrays: hipFree
   std::vector<BaseCsr> base;
   std::vector<DevCSR> table;     // host copy of the device CSR table (base, then derived)
   std::vector<Derived> derived;  // reused by the next snapshot when the source is unchanged
@@ -1209,6 +1210,7 @@ void device_free(Engine& e) {
   if (e.dev) {
     (void)hipSetDevice(e.device);
     free_list(e.dev->allocs);
+    for (void* p : e.dev->hallocs) (void)hipFree(p);
     delete e.dev;
     e.dev = nullptr;
   }
@@ -1447,6 +1449,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     ds->q_bits_deep = 63 - (34 + ceil_log2((uint64_t)md + 1) + ds->node_bits);
   } catch (...) {
     free_list(ds->allocs);
+    for (void* p : ds->hallocs) (void)hipFree(p);
     delete ds;
     throw;
   }
@@ -1473,6 +1476,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     } else {
       free_list(e.dev->allocs);
     }
+    for (void* p : e.dev->hallocs) (void)hipFree(p);
     delete e.dev;
   }
   e.dev = ds;
