@@ -35,8 +35,10 @@ BATCH = 65536
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # a 64K batch takes ~10-20 us of device time with 3 in flight: 200 timed batches keep the
+    # pipeline's fill and drain (a few batches' worth) out of the per-batch figure
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--tuples", type=float, default=1e9, help="graph size (1e9 = BASELINE config)")
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget")
@@ -46,7 +48,7 @@ def parse():
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/pmc_r02.sh, calibrated by tools/gather_probe)")
-    ap.add_argument("--host-steps", type=int, default=20, help="PCIe-inclusive host-buffer steps (0 = skip)")
+    ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="check batches in flight (gck_check_submit on this many streams): the next batch's "
                          "bundles fill the tail of the previous one; 1 = one batch at a time")
@@ -338,7 +340,9 @@ def main():
     # batch's copies overlap the other batches' kernels), and one at a time for reference.
     host_rate = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and args.host_steps > 0:
-        h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot]
+        # (up to 32 of the rotated batches, cycled: pinned host memory per batch is 1.6 MB)
+        n_h = min(len(rot), max(32, args.warmup + 1))
+        h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot[:n_h]]
         ref0 = (outs[args.warmup][0].cpu().numpy(), outs[args.warmup][1].cpu().numpy())
         # the same batches in pinned host memory (gck_host_alloc: DMA straight from / into them)
         p_rot = []

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--batches", type=int, default=400)
     ap.add_argument("--depths", default="1,2,3,4,6,8")
     ap.add_argument("--closure", type=int, default=1)
+    ap.add_argument("--host", action="store_true", help="pinned host buffers (gck_host_alloc) instead of HBM")
     args = ap.parse_args()
     import torch
     from gochugaru_amd.engine import Engine
@@ -43,8 +44,25 @@ def main():
             for _ in range(64)]
     streams = [torch.cuda.Stream(dev) for _ in range(max(depths))]
     torch.cuda.synchronize()
+    if args.host:
+        from gochugaru_amd.engine import ITEM_DTYPE
+        import numpy as np
+        hrot = []
+        for b in rot[:16]:
+            a = eng.host_array(n, ITEM_DTYPE)
+            a[:] = b.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+            hrot.append((a, eng.host_array(n, np.uint8), eng.host_array(n, np.int32)))
 
     def run(depth, nb):
+        if args.host:
+            q = collections.deque()
+            for k in range(nb):
+                if len(q) >= depth:
+                    q.popleft().wait()
+                q.append(eng.submit_into(*hrot[k % len(hrot)]))
+            while q:
+                q.popleft().wait()
+            return
         q = collections.deque()
         for k in range(nb):
             if len(q) >= depth:
