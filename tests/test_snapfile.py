@@ -174,8 +174,8 @@ def test_rejects_inconsistent_csrs(tmp_path, case):
     schema = "definition user {}\ndefinition company { relation founder: user }"
     counts = [4, 3]  # users, companies
     off, nbr, rows = [0, 1, 3, 4], [2, 0, 3, 1], 3
-    if case == "rows":
-        rows, off = 2, [0, 1, 4]
+    if case == "rows":  # more rows than objects of the type
+        rows, off = 4, [0, 1, 3, 4, 4]
     elif case == "offsets":
         off = [0, 3, 1, 4]
     elif case == "neighbour":
