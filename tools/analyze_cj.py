@@ -5,7 +5,7 @@ import sys
 import numpy as np
 
 TICK_US = 0.01
-W = 10  # closure.inc kCjTimingWords
+W = 11  # closure.inc kCjTimingWords
 
 
 def launches(path):
@@ -30,19 +30,18 @@ def main(path):
         t0 = r[:, 0].min()
         spans.append((r[:, 4].max() - t0) * TICK_US)
         recs.append(np.column_stack([(r[:, 0] - t0) * TICK_US, (r[:, 1] - r[:, 0]) * TICK_US,
-                                     (r[:, 8] - r[:, 1]) * TICK_US, (r[:, 9] - r[:, 8]) * TICK_US,
+                                     (r[:, 8] - r[:, 1]) * TICK_US, (r[:, 10] - r[:, 8]) * TICK_US,
+                                     (r[:, 9] - r[:, 10]) * TICK_US,
                                      (r[:, 2] - r[:, 9]) * TICK_US, (r[:, 3] - r[:, 2]) * TICK_US,
                                      (r[:, 4] - r[:, 3]) * TICK_US, (r[:, 4] - t0) * TICK_US,
                                      r[:, 5], r[:, 6], r[:, 7]]))
     a = np.concatenate(recs)
     print(f"launches {len(spans)}  span us (first wave start -> last wave end): {pct(np.array(spans))}")
-    names = ["start offset", "table copy", "items", "slots", "extents", "tasks", "end", "wave end offset"]
+    names = ["start offset", "table copy", "items", "slots", "lists", "extents", "tasks", "end", "wave end offset"]
     for k, nm in enumerate(names):
         print(f"{nm:>16} us  {pct(a[:, k])}")
-    print(f"{'tasks/wave':>16}     {pct(a[:, 8])}")
-    print(f"{'probes/wave':>16}     {pct(a[:, 9])}")
-    slow = a[:, 5] > np.percentile(a[:, 5], 90)
-    print(f"slowest 10% of waves by tasks time: mean tasks {a[slow, 8].mean():.0f} vs all {a[:, 8].mean():.0f}")
+    print(f"{'tasks/wave':>16}     {pct(a[:, 9])}")
+    print(f"{'probes/wave':>16}     {pct(a[:, 10])}")
 
 
 if __name__ == "__main__":
