@@ -69,6 +69,7 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
 struct DeviceSnapshot {
   std::vector<void*> allocs;
   std::vector<void*> hallocs;  // hipExtMallocWithFlags (physically contiguous) arrays: hipFree
+  uint32_t slot_bits = 32;     // user-slot entry width (closure.inc): 24 when every hierarchy has <= 2^24 groups
   std::vector<BaseCsr> base;
   std::vector<DevCSR> table;     // host copy of the device CSR table (base, then derived)
   std::vector<Derived> derived;  // reused by the next snapshot when the source is unchanged
@@ -1941,7 +1942,10 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
     j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
-    hipLaunchKernelGGL(k_closure_join, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
+    if (ds.slot_bits == 24)
+      hipLaunchKernelGGL(k_closure_join<24>, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
+    else
+      hipLaunchKernelGGL(k_closure_join<32>, dim3((n + 64u * kWaves - 1) / (64u * kWaves)), dim3(kBlock), 0, st, c, j);
     HIP_OK(hipGetLastError());
   } else {
     launch_wave_bundles(e, w, c, a, st);
