@@ -13,10 +13,18 @@ timeout -k 10 120 $GP > "$OUT/gather_plain.jsonl"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/gfetch" -o gfetch --output-format csv -- $GP > "$OUT/gather_fetch.jsonl" 2> "$OUT/gather_fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/gwrite" -o gwrite --output-format csv -- $GP > "$OUT/gather_write.jsonl" 2> "$OUT/gather_write.err"
 echo "calibration done"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
+# (the CPU baseline and the host-buffer runs are left out under the tracer: they add minutes and
+# nothing to the kernel statistics)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --host-steps 0 "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
+find "$OUT/kt" -name "*kernel_trace.csv" -delete
+# one batch at a time: every launch alone on the GPU, as the bench's roofline times it
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt1" -o kt1 --output-format csv -- python3 bench.py --no-cpu --host-steps 0 --inflight 1 "$@" > "$OUT/kt1.json" 2> "$OUT/kt1.err"
+find "$OUT/kt1" -name "*kernel_trace.csv" -delete
 echo "kernel trace done"
-SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --host-steps 0 $*"
+# one batch at a time under the counters (each kernel is counted alone anyway)
+SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --no-cpu --host-steps 0 --inflight 1 $*"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- $SHORT > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+echo "fetch pass done"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- $SHORT > "$OUT/write.json" 2> "$OUT/write.err"
 echo "pmc done"
 python3 tools/traffic_summary.py "$OUT" > "$OUT/traffic.json"
