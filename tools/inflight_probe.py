@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--batches", type=int, default=400)
     ap.add_argument("--depths", default="1,2,3,4,6,8")
     ap.add_argument("--closure", type=int, default=1)
+    ap.add_argument("--n", type=int, default=65536, help="checks per batch (small: the host cost per batch)")
     ap.add_argument("--host", action="store_true", help="pinned host buffers (gck_host_alloc) instead of HBM")
     args = ap.parse_args()
     import torch
@@ -38,7 +39,7 @@ def main():
         eng.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr.data_ptr(), nbr.numel(), device=True)
     torch.cuda.synchronize()
     eng.commit_snapshot()
-    n = 65536
+    n = args.n
     rot = [synth.checks(G, n, seed=3000 + k) for k in range(64)]
     outs = [(torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.int32, device=dev))
             for _ in range(64)]
