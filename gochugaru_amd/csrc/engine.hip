@@ -1064,6 +1064,7 @@ __global__ void __launch_bounds__(kBlock) k_final(const DevQuery* __restrict__ q
 
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kBCtrs = 8;  // per-batch stage counters after DevCounters (Workspace::b_ctrs)
+constexpr uint32_t kBDone = 5;  // b_ctrs[kBDone]: the closure join's finished blocks (closure.inc CjArgs::done)
 
 #include "bundle.inc"
 
@@ -1702,8 +1703,6 @@ static void add_counters(Engine& e, Workspace& w, const DevCounters& h) {
   e.stats.bidir_checks += h.bidir;
   e.stats.levels += h.bundle_levels;
   e.stats.bundles += h.bundles;
-  e.stats.closure_checks += h.closure;
-  e.stats.slot_checks += h.slot_checks;
 }
 
 // Runs one batch (n <= max_batch) on the grid-wide path. Returns false on a workspace overflow
@@ -1942,6 +1941,14 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
     j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
+    if (!host_out) {  // the join publishes the batch itself (a host batch's copies come first)
+      j.pub = reinterpret_cast<unsigned*>(w.ctr);
+      j.pub_words = kPubWords;
+      j.h_out = w.d_hpub;
+      j.done = w.b_ctrs + kBDone;
+      j.seq = ++w.pub_seq;
+      w.b_seq = j.seq;
+    }
     // a timed batch's events are the kernel's own start and stop (hipExtLaunchKernel), not markers
     // around its dispatch, so they agree with a profiler's kernel duration
     const dim3 grid((n + 64u * kWaves - 1) / (64u * kWaves)), block(kBlock);
@@ -1960,7 +1967,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
-  publish_launch(w, st);
+  if (!w.b_closure || host_out) publish_launch(w, st);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
@@ -1979,6 +1986,15 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   bm = ms;
   const uint32_t n_cj = w.b_closure ? w.h_bctrs[4] : 0u;
   if (n_cj > n) throw Error(GCK_E_DEVICE, "engine invariant violated: closure-join deferred count");
+  if (w.b_closure) {
+    // the join counts only its task-round checks (DevCounters::closure; usually none, so usually
+    // no atomic): the rest of what it answered came from the slots
+    const unsigned long long tasks = w.h_ctr->closure;
+    if (tasks > n - n_cj) throw Error(GCK_E_DEVICE, "engine invariant violated: closure-join task count");
+    std::lock_guard<std::mutex> lk(e.stats_mu);
+    e.stats.closure_checks += n - n_cj;
+    e.stats.slot_checks += n - n_cj - tasks;
+  }
   if (n_cj > 0) {
     // the checks the closure join left: the wave bundles over its list (the publish zeroed the
     // count on the device: restore it first)
@@ -2094,6 +2110,7 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
   static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
   if (dbg_on && w.dbg) {
+    HIP_OK(hipDeviceSynchronize());
     const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;
     std::vector<uint32_t> h(dbg_words);
     HIP_OK(hipMemcpy(h.data(), w.dbg, dbg_words * 4, hipMemcpyDeviceToHost));
@@ -2110,6 +2127,7 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
     }
   }
   if (timing_env && w.timing) {
+    HIP_OK(hipDeviceSynchronize());  // (a closure join publishes its batch before its last waves end)
     const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
     const size_t cj_words = (size_t)kCjTimingWords * (n / 64 + 1);
     std::vector<unsigned long long> h(timing_words + cj_words);

@@ -192,8 +192,8 @@ struct DevCounters {  // device-side counters, reset per level where noted
   unsigned long long bidir;         // checks evaluated bidirectionally
   unsigned long long bundle_levels; // BFS levels run by bundles (summed over bundles)
   unsigned long long bundles;       // bundles run
-  unsigned long long closure;       // checks answered by the closure-join stage (closure.inc)
-  unsigned long long slot_checks;   // checks the closure join's slot test decided (closure.inc)
+  unsigned long long closure;       // checks the closure join answered in its task rounds (closure.inc;
+                                    // the slot-path count is n - deferred - this, on the host)
   unsigned int cav_requests;        // (caveat instance, check context) pairs recorded for evaluation
   unsigned int cav_errors;          // touched pairs whose evaluation failed
 };

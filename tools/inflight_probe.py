@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--depths", default="1,2,3,4,6,8")
     ap.add_argument("--closure", type=int, default=1)
     ap.add_argument("--n", type=int, default=65536, help="checks per batch (small: the host cost per batch)")
+    ap.add_argument("--split", action="store_true", help="time submit and wait calls separately first")
     ap.add_argument("--host", action="store_true", help="pinned host buffers (gck_host_alloc) instead of HBM")
     args = ap.parse_args()
     import torch
@@ -74,6 +75,34 @@ def main():
         while q:
             q.popleft().wait()
 
+    def split(depth, nb):  # host seconds inside submit / wait calls
+        q = collections.deque()
+        ts = tw = 0.0
+        pc = time.perf_counter
+        for k in range(nb):
+            if len(q) >= depth:
+                t = pc()
+                q.popleft().wait()
+                tw += pc() - t
+            j = k % 64
+            t = pc()
+            q.append(eng.submit(rot[j].data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), device=True,
+                                stream=streams[k % depth].cuda_stream))
+            ts += pc() - t
+        while q:
+            q.popleft().wait()
+        return ts, tw
+
+    if args.split:
+        for d in depths:
+            split(d, 20)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ts, tw = split(d, args.batches)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"inflight {d}: {dt / args.batches * 1e6:.2f} us/batch, submit {ts / args.batches * 1e6:.2f} us, "
+                  f"wait {tw / args.batches * 1e6:.2f} us", flush=True)
     for r in range(args.reps):
         for d in depths:
             run(d, 20)
