@@ -53,6 +53,14 @@ def parse():
                     help="check batches in flight (gck_check_submit on this many streams): the next batch's "
                          "bundles fill the tail of the previous one; 1 = one batch at a time")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--driver", default="native", choices=["native", "python"],
+                    help="who runs the submit/wait loop over the device batches: native = the compiled loop "
+                         "of libgck_driver.so (what a cgo caller runs), python = one ctypes call per submit/wait")
+    ap.add_argument("--engine-streams", type=int, default=0,
+                    help="1: device batches run on the engine's workspace streams (GCK_SUBMIT_ENGINE_STREAM) "
+                         "instead of the caller's streams")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0 = the runtime's default, 4)")
     ap.add_argument("--bundle-checks", type=int, default=0)
     ap.add_argument("--bundle-frontier", type=int, default=0)
     ap.add_argument("--bundle-visited", type=int, default=0)
@@ -188,6 +196,8 @@ def progress(msg):
 
 def main():
     args = parse()
+    if args.hw_queues:  # before the HIP runtime starts
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
 
@@ -211,7 +221,9 @@ def main():
 
     t0 = time.time()
     depth = max(1, args.inflight)
-    eng = Engine(device=local, profile=not args.no_profile, workspaces=max(2, depth),
+    # events only for the solo phase after the timed region (and the configs timed without one)
+    solo_profile = WL.kind not in ("mixed", "quota") and not args.partitioned
+    eng = Engine(device=local, profile=not args.no_profile and not solo_profile, workspaces=max(2, depth),
                  max_batch=args.batch * world if args.partitioned else args.batch, wide_only=args.wide_only,
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
@@ -231,10 +243,13 @@ def main():
     dev_bytes = eng.device_bytes
 
     stream = torch.cuda.current_stream(dev).cuda_stream
+    run_steps = None  # the nested workload's compiled submit/wait loop (--driver native)
     if args.partitioned:
         # one global batch: every rank's 64K checks, the same items on every rank
-        from gochugaru_amd.partition import PartitionedChecker
-        pc = PartitionedChecker(eng)
+        from gochugaru_amd.partition import PartitionedChecker, RcclPartitionedChecker
+        # nccl: the level loop and its RCCL exchange inside libgck (gck_part_check); else the
+        # Python driver over torch.distributed (gloo rehearsals)
+        pc = RcclPartitionedChecker(eng) if args.part_backend == "nccl" else PartitionedChecker(eng)
         items = torch.cat([WL.checks(args.batch, 1000 + r) for r in range(world)])
         n_global = args.batch * world
         out = {}
@@ -297,14 +312,31 @@ def main():
             if len(pending) >= depth:
                 pending.popleft().wait()
             pending.append(eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
-                                      device=True, stream=streams[k % depth].cuda_stream))
+                                      device=True, stream=streams[k % depth].cuda_stream,
+                                      engine_stream=bool(args.engine_streams)))
 
         def drain():
             while pending:
                 pending.popleft().wait()
 
-    for _ in range(args.warmup):
-        step()
+        if args.driver == "native":
+            # the same submit/wait loop, run by the compiled caller (libgck_driver.so) over the
+            # steps of one phase: run_steps(count) checks the next `count` rotated batches
+            def run_steps(count):
+                k0 = cursor["k"]
+                cursor["k"] += count
+                ks = range(k0, k0 + count)
+                eng.run_device_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
+                                       [outs[k][1].data_ptr() for k in ks], args.batch, depth,
+                                       [streams[(k - k0) % depth].cuda_stream for k in ks],
+                                       engine_streams=bool(args.engine_streams))
+
+    native = run_steps is not None
+    if native:
+        run_steps(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
     if WL.kind not in ("mixed", "quota") and not args.partitioned:
         drain()
     torch.cuda.synchronize()
@@ -313,8 +345,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if native:
+        run_steps(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
     if WL.kind not in ("mixed", "quota") and not args.partitioned:
         drain()
     torch.cuda.synchronize()
@@ -333,12 +368,14 @@ def main():
     # hold, so the roofline uses these; `achieved_job` is the whole timed region.
     st_solo = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and not args.no_profile:
+        eng.set_profile(True)  # the timed region ran without events (a timed launch holds back the others)
         eng.reset_stats()
         for k in range(min(len(rot), 48)):
             eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(), device=True,
                        stream=streams[0].cuda_stream).wait()
         torch.cuda.synchronize()
         st_solo = eng.stats()
+        eng.set_profile(False)
         progress("solo launches done")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -480,6 +517,9 @@ def main():
                 # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)
                 "achieved_job": round(b_alg * args.steps / elapsed / 1e9, 3),
                 "inflight": depth,
+                "driver": args.driver if run_steps is not None or args.driver == "python" else "python",
+                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or 4,
+                "engine_streams": bool(args.engine_streams),
                 "launch_timing": "solo" if st_solo is not None else "timed region",
                 "alg_counts": {k: int(v) for k, v in cnt.items()},
                 "mean_launch_ms": {"stage A (k_closure_join + k_bundles<1>)": round(ms_a, 4),

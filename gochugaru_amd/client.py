@@ -27,7 +27,7 @@ from . import rel as _rel
 from .consistency import Background, Context, Strategy
 from .engine import (CONSISTENCY_AT_LEAST, CONSISTENCY_FULL, CONSISTENCY_MIN_LATENCY,
                      CONSISTENCY_SNAPSHOT, ELLIPSIS, GCK_E_DEVICE, GCK_E_NOT_FOUND, GCK_E_REVISION,
-                     ID_ABSENT, ITEM_ERROR_MESSAGES, PERM_HAS, REL_INVALID, TYPE_INVALID, Engine,
+                     ID_ABSENT, ID_WILDCARD, ITEM_ERROR_MESSAGES, PERM_HAS, REL_INVALID, TYPE_INVALID, Engine,
                      GckError)
 
 CHECK_ITER_CHUNK = 1000  # client/client.go:166
@@ -224,7 +224,8 @@ class Client:
     def LookupSubjects(self, ctx: Optional[Context], cs: Optional[Strategy], resource: str, permission: str,
                        subject: str) -> Iterator[Tuple[str, Optional[Exception]]]:
         """``client/client.go:560-599``: yields the ids of the subjects of type ``subject``
-        ("user" or "team#member") that have ``permission`` on ``resource`` ("document:README")."""
+        ("user" or "team#member") that have ``permission`` on ``resource`` ("document:README");
+        a wildcard grant yields "*" once (as SpiceDB streams it), not every subject of the type."""
         self.checkOverlap(ctx)
         try:
             res_type, res_id, _ = _rel.ParseObjectSet(resource)
@@ -240,7 +241,8 @@ class Client:
             rid = int(eng.intern(rt, [res_id])[0])
             ids, _ = retryRetriableErrors(ctx or Background, lambda: eng.lookup_subjects(
                 rt, rid, perm, st, srel, requirement, revision)) if rid != ID_ABSENT else ([], [])
-            names = [eng.object_name(st, int(i)) for i in ids]
+            # a wildcard grant is the subject "*" (SpiceDB's LookupSubjects result for `type:*`)
+            names = ["*" if int(i) == ID_WILDCARD else eng.object_name(st, int(i)) for i in ids]
         except Exception as e:  # noqa: BLE001
             yield "", e
             return

@@ -1,0 +1,52 @@
+// driver.cpp — a compiled caller of the C ABI's asynchronous batches: the loop a cgo host runs
+// (submit, keep `depth` batches in flight, wait for the oldest), so that bench.py can time the
+// engine through C calls instead of one ctypes round trip per call (~3-4 us each in CPython,
+// ~0.1 us through cgo). It calls only gck_check_submit / gck_check_wait, through the pointers the
+// caller passes (the entry points of the libgck instance that created the engine), so it never
+// links a second copy of the library.
+//   built by make -C gochugaru_amd/csrc as gochugaru_amd/libgck_driver.so
+#include <chrono>
+#include <cstdint>
+#include <deque>
+
+#include "gck.h"
+
+using submit_fn = int (*)(gck_engine*, const gck_consistency*, const gck_item*, size_t, const char* const*,
+                          const size_t*, size_t, int64_t, uint8_t*, int32_t*, uint32_t, void*, gck_batch**);
+using wait_fn = int (*)(gck_engine*, gck_batch*);
+
+extern "C" {
+
+// Runs batches k = 0 .. n_batches-1 (device buffers items[k], perm[k], err[k], n checks each) with
+// up to `depth` in flight; batch k is submitted on streams[k % depth] with GCK_SUBMIT_DEVICE | flags
+// (GCK_SUBMIT_ENGINE_STREAM: on the engine's workspace streams instead). Returns GCK_OK or the first
+// error; *seconds = wall time from the first submit to the last wait.
+int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs, size_t n_batches, const uint64_t* items,
+             const uint64_t* perm, const uint64_t* err, size_t n, uint32_t depth, const uint64_t* streams,
+             uint32_t flags, double* seconds) {
+  if (depth == 0) depth = 1;
+  std::deque<gck_batch*> q;
+  int rc = GCK_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t k = 0; k < n_batches && rc == GCK_OK; ++k) {
+    if (q.size() >= depth) {
+      rc = wait(e, q.front());
+      q.pop_front();
+      if (rc != GCK_OK) break;
+    }
+    gck_batch* b = nullptr;
+    rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, 0,
+                reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), GCK_SUBMIT_DEVICE | flags,
+                reinterpret_cast<void*>(streams[k % depth]), &b);
+    if (rc == GCK_OK) q.push_back(b);
+  }
+  while (!q.empty()) {  // every submitted batch is waited for, also after an error
+    const int r = wait(e, q.front());
+    if (rc == GCK_OK) rc = r;
+    q.pop_front();
+  }
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+}  // extern "C"

@@ -2535,11 +2535,11 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
 }
 
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                   int32_t* err, void* stream, bool host, CavCall cav) {
+                   int32_t* err, void* stream, bool host, bool engine_stream, CavCall cav) {
   HIP_OK(hipSetDevice(e.device));
   std::lock_guard<std::mutex> lk(w->m);
   if (n > w->max_batch) throw Error(GCK_E_INVALID_ARGUMENT, "submitted batch above max_batch");
-  hipStream_t st = host ? w->stream : (hipStream_t)stream;
+  hipStream_t st = (host || engine_stream) ? w->stream : (hipStream_t)stream;
   stage_caveats(*w, std::move(cav), st);
   if (now_us == 0) now_us = wall_now_us();
   submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host);

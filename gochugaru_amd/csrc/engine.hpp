@@ -243,7 +243,7 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
 // the caller then releases the workspace. `items` etc. are device pointers on `stream`
 // (host == false) or host buffers (host == true: the workspace's own stream).
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
-                   int32_t* err, void* stream, bool host, CavCall cav);
+                   int32_t* err, void* stream, bool host, bool engine_stream, CavCall cav);
 void device_wait(Engine& e, Workspace* w);
 // Pinned host buffers (gck_host_alloc): a host batch whose items / results live in one is
 // copied by DMA directly, without the workspace's staging copy.
@@ -259,6 +259,8 @@ void device_export(Engine& e, std::vector<HostCSR>& out);
 // vary_res, else subject id); matching ids ascending with their permissionship
 void device_lookup(Engine& e, Workspace& w, const gck_item& proto, bool vary_res, uint32_t n_candidates,
                    int64_t now_us, std::vector<uint32_t>& ids, std::vector<uint8_t>& perms);
+void device_lookup_subjects(Engine& e, Workspace& w, const gck_item& proto, int64_t now_us, std::vector<uint32_t>& ids,
+                            std::vector<uint8_t>& perms);
 // partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
 void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
 void part_expand(Engine& e, uint64_t* send_counts);

@@ -722,7 +722,7 @@ int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* 
     try {
       std::shared_lock<std::shared_mutex> lk(e.mu);
       check_request(e, cs, items, n, host, contexts, context_lens, n_contexts);
-      device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host,
+      device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host, !host && (flags & GCK_SUBMIT_ENGINE_STREAM),
                     caveat_call(e, contexts, context_lens, n_contexts));
     } catch (...) {
       release_ws(e, w);
@@ -905,8 +905,12 @@ static void lookup(gck_engine* ge, const gck_consistency* cs, const gck_item& pr
                    std::memcmp(&g_lookup.proto, &proto, sizeof(gck_item)) == 0;
   if (!hit) {
     g_lookup.generation = 0;
-    const uint32_t n = e.interner[vary_res ? proto.resource_type : proto.subject_type].count;
-    device_lookup(e, *lease.w, proto, vary_res, n, now_us, g_lookup.ids, g_lookup.perms);
+    if (vary_res) {
+      device_lookup(e, *lease.w, proto, true, e.interner[proto.resource_type].count, now_us, g_lookup.ids,
+                    g_lookup.perms);
+    } else {
+      device_lookup_subjects(e, *lease.w, proto, now_us, g_lookup.ids, g_lookup.perms);
+    }
     g_lookup.generation = e.generation;
     g_lookup.proto = proto;
     g_lookup.vary_res = vary_res;
@@ -948,6 +952,15 @@ int gck_last_stats(gck_engine* ge, gck_stats* out) {
     Engine& e = need(ge);
     REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
     *out = e.stats;
+  });
+}
+
+int gck_set_profile(gck_engine* ge, uint32_t on) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::unique_lock<std::shared_mutex> lk(e.mu);  // no batch is being submitted
+    if (on) e.cfg.flags |= GCK_FLAG_PROFILE;
+    else e.cfg.flags &= ~GCK_FLAG_PROFILE;
   });
 }
 

@@ -59,6 +59,7 @@ FLAG_NO_CLOSURE = 32
 FLAG_LAZY_CAVEATS = 64
 FLAG_NO_SLOTS = 128
 SUBMIT_DEVICE = 1
+SUBMIT_ENGINE_STREAM = 2
 
 ITEM_DTYPE = np.dtype([
     ("resource_type", "<u2"), ("permission", "<u2"), ("resource_id", "<u4"),
@@ -171,6 +172,7 @@ _SIGS = {
     "gck_check_submit": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.POINTER(C.c_char_p),
                                    C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P, C.c_uint32, _P,
                                    C.POINTER(_P)]),
+    "gck_set_profile": (C.c_int, [_P, C.c_uint32]),
     "gck_check_wait": (C.c_int, [_P, _P]),
     "gck_host_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
     "gck_host_free": (C.c_int, [_P, _P]),
@@ -196,6 +198,24 @@ _SIGS = {
 }
 
 _lib = None
+
+
+_DRIVER = None
+
+
+def _driver():
+    """libgck_driver.so (csrc/driver.cpp): the compiled submit/wait loop bench.py times through."""
+    global _DRIVER
+    if _DRIVER is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgck_driver.so")
+        if not os.path.exists(path):
+            raise OSError(f"{path} is missing: build it with `make -C gochugaru_amd/csrc`")
+        d = C.CDLL(path)
+        d.gckd_run.restype = C.c_int
+        d.gckd_run.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                               C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]
+        _DRIVER = d
+    return _DRIVER
 
 
 def load_library(path: str = _LIB_PATH):
@@ -462,7 +482,7 @@ class Engine:
 
     def submit(self, items, n: Optional[int] = None, out_perm=None, out_err=None, requirement: int = CONSISTENCY_MIN_LATENCY,
                revision: int = 0, now_us: int = 0, contexts: Optional[Sequence] = None, device: bool = False,
-               stream: Optional[int] = None) -> "Batch":
+               stream: Optional[int] = None, engine_stream: bool = False) -> "Batch":
         """Starts one batch (n <= max_batch) without waiting (gck_check_submit); Batch.wait()
         completes it. Host batches: `items` is an ITEM_DTYPE array and the results are returned by
         wait(). Device batches (device=True): `items`, `out_perm`, `out_err` are device pointers
@@ -471,8 +491,9 @@ class Engine:
         ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
         h = _P()
         if device:
+            flags = SUBMIT_DEVICE | (SUBMIT_ENGINE_STREAM if engine_stream else 0)
             _check(self._lib.gck_check_submit(self._h, C.byref(cs), items, n, ctx_arr, ctx_lens, n_ctx, now_us,
-                                              out_perm, out_err, SUBMIT_DEVICE, stream, C.byref(h)))
+                                              out_perm, out_err, flags, stream, C.byref(h)))
             return Batch(self, h, None, None, None)
         items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
         n = len(items)
@@ -506,6 +527,27 @@ class Engine:
                                           err.ctypes.data if n else None, 0, None, C.byref(h)))
         return Batch(self, h, perm, err, items)
 
+    def set_profile(self, on: bool):
+        """GCK_FLAG_PROFILE for the batches submitted from now on (gck_set_profile)."""
+        _check(self._lib.gck_set_profile(self._h, 1 if on else 0))
+
+    def run_device_batches(self, items, perms, errs, n: int, depth: int, streams, engine_streams: bool = False) -> float:
+        """Checks len(items) device batches of n items each (device pointers items[k], perms[k],
+        errs[k]) with up to `depth` in flight, batch k on streams[k % depth] (engine_streams: on
+        the engine's workspace streams, GCK_SUBMIT_ENGINE_STREAM), through the compiled
+        submit/wait loop of libgck_driver.so (the loop a cgo caller runs; no Python per batch).
+        Returns the loop's wall time in seconds."""
+        drv = _driver()
+        k = len(items)
+        arr = lambda xs: (C.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
+        cs = _Consistency(CONSISTENCY_MIN_LATENCY, 0, 0)
+        secs = C.c_double(0.0)
+        submit = C.cast(self._lib.gck_check_submit, C.c_void_p)
+        wait = C.cast(self._lib.gck_check_wait, C.c_void_p)
+        _check(drv.gckd_run(submit, wait, self._h, C.byref(cs), k, arr(items), arr(perms), arr(errs), n, depth,
+                            arr(streams), SUBMIT_ENGINE_STREAM if engine_streams else 0, C.byref(secs)))
+        return secs.value
+
     # ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) --------
     def _lookup(self, fn, args, requirement, revision):
         cs = _Consistency(requirement, 0, revision)
@@ -535,7 +577,8 @@ class Engine:
     def lookup_subjects(self, resource_type: int, resource_id: int, permission: int, subject_type: int,
                         subject_relation: int = ELLIPSIS, requirement: int = CONSISTENCY_MIN_LATENCY,
                         revision: int = 0, now_us: int = 0) -> Tuple[np.ndarray, np.ndarray]:
-        """Ids (ascending) of the subject_type subjects that have `permission` on the resource."""
+        """Ids (ascending) of the subject_type subjects that have `permission` on the resource;
+        a wildcard grant is one id, ID_WILDCARD (last), instead of every subject of the type."""
         now_us = now_us or time.time_ns() // 1000
         return self._lookup(self._lib.gck_lookup_subjects,
                             (resource_type, resource_id, permission, subject_type, subject_relation, now_us),

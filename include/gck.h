@@ -328,9 +328,14 @@ int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
  * out_err are device buffers ordered on `stream` (as gck_check_bulk_device_ctx); otherwise they
  * are host buffers (the items are staged before the call returns; the outputs are written by the
  * wait). Consistency is checked at submit; the batch sees the snapshot current at submit, even if
- * a Watch batch is applied before the wait. */
+ * a Watch batch is applied before the wait. GCK_SUBMIT_DEVICE | GCK_SUBMIT_ENGINE_STREAM: device
+ * buffers, but the batch runs on the stream of the workspace it holds (created by the engine, one
+ * per workspace, so that batches in flight sit on distinct hardware queues) and `stream` is
+ * ignored: the items must be complete when the call is made, and the results are complete when
+ * gck_check_wait returns. */
 typedef struct gck_batch gck_batch;
 #define GCK_SUBMIT_DEVICE 1u
+#define GCK_SUBMIT_ENGINE_STREAM 2u
 int gck_check_submit(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
                      const char* const* contexts, const size_t* context_lens, size_t n_contexts,
                      int64_t now_us, uint8_t* out_perm, int32_t* out_err, uint32_t flags, void* stream,
@@ -343,6 +348,9 @@ int gck_host_alloc(gck_engine* e, size_t bytes, void** out);
 int gck_host_free(gck_engine* e, void* p);
 int gck_last_stats(gck_engine* e, gck_stats* out);
 int gck_reset_stats(gck_engine* e);
+/* Turns GCK_FLAG_PROFILE on or off for the batches submitted from now on (a timed batch brackets
+ * its stage A with the kernel's own start/stop events, every 4th batch of a workspace). */
+int gck_set_profile(gck_engine* e, uint32_t on);
 
 /* ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) -------- */
 /* Ids of the `resource_type` objects on which the subject has `permission` — HAS or CONDITIONAL,
@@ -356,8 +364,10 @@ int gck_lookup_resources(gck_engine* e, const gck_consistency* cs, uint16_t reso
                          uint16_t subject_type, uint16_t subject_relation, uint32_t subject_id, int64_t now_us,
                          uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);
 /* Ids of the `subject_type` objects (with `subject_relation`, GCK_ELLIPSIS for plain objects)
- * that have `permission` on one resource, ascending; same protocol. Concrete subjects only: a
- * wildcard grant makes every subject of the type match (SpiceDB reports it as the subject "*"). */
+ * that have `permission` on one resource, ascending; same protocol. As SpiceDB's LookupSubjects:
+ * the candidates are the subjects on the relationships the permission's rewrite reaches from the
+ * resource (a walk on the device), each checked on the check path; a wildcard grant is reported
+ * once, as GCK_ID_WILDCARD (last), not as every subject of the type. */
 int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resource_type, uint32_t resource_id,
                         uint16_t permission, uint16_t subject_type, uint16_t subject_relation, int64_t now_us,
                         uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);

@@ -1023,6 +1023,57 @@ class Checker:
     def check_many(self, items) -> List[Tuple[int, int]]:
         return [self.check(it) for it in items]
 
+    def lookup_subjects(self, rtype, rid, perm, stype, srel=ELLIPSIS, context=None) -> List[Tuple[str, int]]:
+        """``Client.LookupSubjects`` (``client/client.go:560-599``) as SpiceDB answers it: the
+        subjects of kind (stype, srel) that have ``perm`` on rtype:rid — HAS or CONDITIONAL —
+        sorted by id, with a wildcard grant reported once as the subject ``"*"`` (last). The
+        candidates are the concrete subjects on the relationships the rewrite's positive operands
+        reach from the resource (union and intersection operands, exclusion bases, computed
+        usersets, arrows, userset subjects; expired relationships skipped); each is checked, and
+        so is one subject that appears nowhere, which stands for the wildcard. Any candidate's
+        depth error fails the lookup (ValueError)."""
+        found, seen = set(), set()
+        todo = [(rtype, rid, perm)]
+        while todo:
+            t, i, r = todo.pop()
+            if (t, i, r) in seen:
+                continue
+            seen.add((t, i, r))
+            rel = self.schema.relation(t, r)
+            if rel is None:
+                continue
+            if not rel.is_permission:
+                for tu in self.store.get(t, i, r):
+                    if not self._visible(tu) or tu.subject_id == WILDCARD:
+                        continue
+                    if tu.subject_type == stype and tu.subject_relation == srel:
+                        found.add(tu.subject_id)
+                    if tu.subject_relation != ELLIPSIS:
+                        todo.append((tu.subject_type, tu.subject_id, tu.subject_relation))
+                continue
+            exprs = [rel.expr]
+            while exprs:
+                e = exprs.pop()
+                if e.op in ("union", "intersect"):
+                    exprs.extend(e.children)
+                elif e.op == "exclude":
+                    exprs.append(e.children[0])
+                elif e.op == "computed":
+                    todo.append((t, i, e.name))
+                elif e.op == "arrow":
+                    for tu in self.store.get(t, i, e.tupleset):
+                        if self._visible(tu):
+                            todo.append((tu.subject_type, tu.subject_id, e.name))
+        out = []
+        cands = sorted(found) + ([None] if srel == ELLIPSIS else [])
+        for sid in cands:
+            p, err = self.check(Item(rtype, rid, perm, stype, "\x00absent" if sid is None else sid, srel, context))
+            if err == ITEM_ERR_MAX_DEPTH:
+                raise ValueError("max depth exceeded")
+            if p in (HAS, COND):
+                out.append((WILDCARD if sid is None else sid, p))
+        return out
+
     # -- SpiceDB restatement -------------------------------------------------------------
     def _dispatch(self, rtype, rid, rel, depth_remaining) -> int:
         if depth_remaining <= 0:

@@ -9,6 +9,7 @@ from gochugaru_amd import engine as E
 from gochugaru_amd.client import Client
 from tests import gen
 from tests.helpers import load_golden, oracle_for
+from tests.lookup_cases import WILD_CASES, WILD_SCHEMA
 from oracle import spicedb_ref as ref
 
 pytestmark = pytest.mark.gpu
@@ -80,8 +81,36 @@ def test_lookup_parity(family, seed, path):
                                         E.ELLIPSIS, int(e.intern(e.type_id(stype), [sid])[0]), now_us=gen.NOW_US)
         assert list(zip(ids.tolist(), perms.tolist())) == want, c
         rid = rest.split("#", 1)[0]
-        want = _oracle_lookup(ck, e, stype, lambda n: ref.Item(rtype, rid, perm, stype, n), False)
+        want = ck.lookup_subjects(rtype, rid, perm, stype)
         ids, perms = e.lookup_subjects(e.type_id(rtype), int(e.intern(e.type_id(rtype), [rid])[0]),
                                        e.relation_id(e.type_id(rtype), perm), e.type_id(stype), now_us=gen.NOW_US)
-        assert list(zip(ids.tolist(), perms.tolist())) == want, c
+        got = [("*" if i == E.ID_WILDCARD else e.object_name(e.type_id(stype), i), p)
+               for i, p in zip(ids.tolist(), perms.tolist())]
+        assert sorted(got) == sorted(want), c
+        # every subject the candidate sweep finds is reported, or folded into "*"
+        sweep = _oracle_lookup(ck, e, stype, lambda n: ref.Item(rtype, rid, perm, stype, n), False)
+        named = {n for n, _ in got}
+        assert all(e.object_name(e.type_id(stype), i) in named or "*" in named for i, _ in sweep), c
+    e.close()
+
+
+@pytest.mark.parametrize("case", range(len(WILD_CASES)))
+@pytest.mark.parametrize("path", ["bundle", "wide"])
+def test_lookup_subjects_wildcard(case, path):
+    """LookupSubjects reports a wildcard grant as the subject "*" (client/client.go:560-599 yields
+    SubjectObjectId), beside the concrete subjects the walk meets; hand-derived answers, also the
+    oracle's (tests/test_oracle.py)."""
+    tuples, perm, kind, want = WILD_CASES[case]
+    e = make_engine(WILD_SCHEMA, tuples + ["doc:other#viewer@user:zed", "group:h#member@user:yan"],
+                    **({"wide_only": True} if path == "wide" else {}))
+    c = Client(e)
+    got = sorted(s for s, err in c.LookupSubjects(None, consistency.MinLatency(), "doc:d", perm, kind))
+    assert got == sorted(n for n, _ in want)
+    st, _, srel = kind.partition("#")
+    tid = e.type_id(st)
+    ids, perms = e.lookup_subjects(e.type_id("doc"), int(e.intern(e.type_id("doc"), ["d"])[0]),
+                                   e.relation_id(e.type_id("doc"), perm), tid,
+                                   e.relation_id(tid, srel) if srel else E.ELLIPSIS)
+    named = sorted(("*" if i == E.ID_WILDCARD else e.object_name(tid, i), p) for i, p in zip(ids.tolist(), perms.tolist()))
+    assert named == sorted(want)
     e.close()

@@ -3,6 +3,7 @@ the hand-derived SpiceDB-semantics fixtures. CPU only."""
 import pytest
 
 from oracle import spicedb_ref as ref
+from tests.lookup_cases import WILD_CASES, WILD_SCHEMA
 from tests.helpers import (expected_code, iso_to_unix, load_golden, oracle_for, parse_check,
                            to_oracle_item)
 
@@ -117,3 +118,14 @@ def test_lookup_resources_known_answers():
         stype, sid = case["subject"].split(":")
         got = [d for d in docs if ck.check(ref.Item(typ, d, perm, stype, sid))[0] == ref.HAS]
         assert got == case["expected"], case["name"]
+
+
+@pytest.mark.parametrize("case", range(len(WILD_CASES)))
+def test_lookup_subjects_wildcard(case):
+    """The oracle's LookupSubjects on the hand-derived wildcard cases (parity unpinned by the
+    reference: its only LookupSubjects-shaped vectors are client_test.go's LookupResources ones)."""
+    tuples, perm, kind, want = WILD_CASES[case]
+    ck = oracle_for(WILD_SCHEMA, tuples + ["doc:other#viewer@user:zed", "group:h#member@user:yan"])
+    st, _, srel = kind.partition("#")
+    got = ck.lookup_subjects("doc", "d", perm, st, srel or ref.ELLIPSIS)
+    assert sorted(got) == sorted(want)
