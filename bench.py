@@ -35,10 +35,12 @@ BATCH = 65536
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # a 64K batch takes ~10-20 us of device time with 3 in flight: 200 timed batches keep the
-    # pipeline's fill and drain (a few batches' worth) out of the per-batch figure
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # a 64K batch takes ~6 us of device time with 12 in flight: 2000 timed batches (~12 ms) keep
+    # the pipeline's fill and drain (a few batches' worth) and host jitter out of the figure
+    # (configs 2, 3, 5: 200 / 20 — their steps are longer and config 5 pre-generates a Watch
+    # batch or 64K contexts per step)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--tuples", type=float, default=1e9, help="graph size (1e9 = BASELINE config)")
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget")
@@ -49,14 +51,15 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/pmc_r02.sh, calibrated by tools/gather_probe)")
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="check batches in flight (gck_check_submit on this many streams): the next batch's "
-                         "bundles fill the tail of the previous one; 1 = one batch at a time")
+                         "kernels fill the tail of the previous one; 1 = one batch at a time (default: 12 for "
+                         "config 4, 3 for the others)")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="who runs the submit/wait loop over the device batches: native = the compiled loop "
                          "of libgck_driver.so (what a cgo caller runs), python = one ctypes call per submit/wait")
-    ap.add_argument("--engine-streams", type=int, default=0,
+    ap.add_argument("--engine-streams", type=int, default=1,
                     help="1: device batches run on the engine's workspace streams (GCK_SUBMIT_ENGINE_STREAM) "
                          "instead of the caller's streams")
     ap.add_argument("--hw-queues", type=int, default=0,
@@ -83,7 +86,15 @@ def parse():
                          "config 5 with 32K per-relationship caveat contexts x one context per request")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
-    return ap.parse_args()
+    args = ap.parse_args()
+    nested = args.config == "nested"
+    if args.steps is None:
+        args.steps = 2000 if nested else 200
+    if args.warmup is None:
+        args.warmup = 100 if nested else 20
+    if args.inflight is None:
+        args.inflight = 12 if nested else 3
+    return args
 
 
 class Workload:

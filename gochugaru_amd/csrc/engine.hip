@@ -1953,10 +1953,15 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     // around its dispatch, so they agree with a profiler's kernel duration
     const dim3 grid((n + 64u * kWaves - 1) / (64u * kWaves)), block(kBlock);
     hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
-    if (ds.slot_bits == 24)
-      hipExtLaunchKernelGGL(k_closure_join<24>, grid, block, 0, st, e0, e1, 0, c, j);
+    const bool small = j.table_bytes <= kCjLdsBytesSmall;
+    if (ds.slot_bits == 24 && small)
+      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
+    else if (ds.slot_bits == 24)
+      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytes>), grid, block, 0, st, e0, e1, 0, c, j);
+    else if (small)
+      hipExtLaunchKernelGGL((k_closure_join<32, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
     else
-      hipExtLaunchKernelGGL(k_closure_join<32>, grid, block, 0, st, e0, e1, 0, c, j);
+      hipExtLaunchKernelGGL((k_closure_join<32, kCjLdsBytes>), grid, block, 0, st, e0, e1, 0, c, j);
     HIP_OK(hipGetLastError());
   } else {
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev0, st));

@@ -147,3 +147,23 @@ def test_rccl_loop_single_rank_matches_oracle(family, seed):
     perm2, err2 = pc.check(d_items, len(items), now_us=gen.NOW_US)  # the communicator is reused
     assert perm2.cpu().tolist() == perm.cpu().tolist() and err2.cpu().tolist() == err.cpu().tolist()
     e.close()
+
+
+def test_partitioned_steps_refuse_a_swapped_snapshot():
+    """A Watch batch between gck_part_begin and a later step swaps the device snapshot: the step
+    fails with GCK_E_STATE instead of running on other (or freed) arrays; a new begin works."""
+    schema, tuples, checks = gen.FAMILIES["gdocs"](1)
+    e = E.Engine(device=0)
+    e.set_partition(0, 1)
+    e.load_schema(schema)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    items = e.make_items([parse_check(c) for c in checks[:64]])
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    e.part_begin(d_items.data_ptr(), len(items))
+    e.apply_updates_text(2, "TOUCH " + tuples[0])
+    with pytest.raises(E.GckError) as ei:
+        e.part_expand()
+    assert ei.value.code == E.GCK_E_STATE
+    e.part_begin(d_items.data_ptr(), len(items))
+    e.part_expand()
+    e.close()
