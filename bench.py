@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="check batches in flight (gck_check_submit on this many streams): the next batch's "
-                         "kernels fill the tail of the previous one; 1 = one batch at a time (default: 12 for "
+                         "kernels fill the tail of the previous one; 1 = one batch at a time (default: 16 for "
                          "config 4, 3 for the others)")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
@@ -93,7 +93,7 @@ def parse():
     if args.warmup is None:
         args.warmup = 100 if nested else 20
     if args.inflight is None:
-        args.inflight = 12 if nested else 3
+        args.inflight = 16 if nested else 3
     return args
 
 

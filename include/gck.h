@@ -139,7 +139,10 @@ typedef struct gck_config {
   uint32_t bidir_both;         /* bidirectional checks expand both sides while their two
                                   frontiers hold at most this many entries; 0 = 64 */
   uint32_t workspaces;         /* check batches in flight at once (concurrent callers and
-                                  submitted batches), one device workspace each; 0 = 4 */
+                                  submitted batches), one device workspace each; 0 = 4. A
+                                  submit waits for a free workspace: one thread must keep at
+                                  most this many batches outstanding. Config 4 peaks at ~16
+                                  in flight */
 } gck_config;
 
 /* One check item, interned: CheckBulkPermissionsRequestItem (client/client.go:244-258). */
