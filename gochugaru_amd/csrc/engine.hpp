@@ -187,7 +187,6 @@ struct Engine {
   std::condition_variable ws_cv;
   std::vector<Workspace*> ws_pool;
   Workspace* part_ws = nullptr;   // the partitioned batch's own workspace (partition.inc)
-  uint64_t part_gen = 0;          // the snapshot generation its gck_part_begin saw (later steps must match)
   uint64_t part_generation = 0;   // the snapshot generation a partitioned batch started on
   void* part_comm = nullptr;      // ncclComm_t of gck_part_init (partition.inc)
   std::mutex stats_mu;            // stats are added by concurrent batches

@@ -783,13 +783,6 @@ uint32_t gck_partition_owner(uint32_t object_id, uint32_t world) {
   return world <= 1 ? 0u : part_owner(object_id, world);
 }
 
-// A partitioned check's steps are separate calls: a Watch batch or snapshot between them would
-// swap the device snapshot under the later steps, so they refuse to run on another generation.
-static void same_part_snapshot(const Engine& e) {
-  REQUIRE(e.part_gen == e.generation, GCK_E_STATE,
-          "the snapshot changed during a partitioned check: start it again with gck_part_begin");
-}
-
 int gck_part_begin(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us, void* stream) {
   return guard([&] {
     Engine& e = need(ge);
@@ -797,7 +790,6 @@ int gck_part_begin(gck_engine* ge, const gck_item* d_items, size_t n, int64_t no
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || d_items, GCK_E_INVALID_ARGUMENT, "null items");
     part_begin(e, d_items, n, now_us, stream);
-    e.part_gen = e.generation;
   });
 }
 
@@ -806,7 +798,6 @@ int gck_part_expand(gck_engine* ge, uint64_t* send_counts) {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(send_counts, GCK_E_INVALID_ARGUMENT, "null counts");
-    same_part_snapshot(e);
     part_expand(e, send_counts);
   });
 }
@@ -816,7 +807,6 @@ int gck_part_pack(gck_engine* ge, void* d_send, size_t send_cap) {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
     REQUIRE(d_send || !send_cap, GCK_E_INVALID_ARGUMENT, "null buffer");
-    same_part_snapshot(e);
     part_pack(e, d_send, send_cap);
   });
 }
@@ -825,7 +815,6 @@ int gck_part_ingest(gck_engine* ge, const void* d_recv, size_t n_recv, void* d_f
   return guard([&] {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
-    same_part_snapshot(e);
     REQUIRE(d_flags && (d_recv || !n_recv), GCK_E_INVALID_ARGUMENT, "null buffers");
     part_ingest(e, d_recv, n_recv, d_flags);
   });
@@ -835,7 +824,6 @@ int gck_part_resolve(gck_engine* ge, const void* d_flags, uint32_t* out_active) 
   return guard([&] {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
-    same_part_snapshot(e);
     REQUIRE(d_flags && out_active, GCK_E_INVALID_ARGUMENT, "null argument");
     *out_active = part_resolve(e, d_flags);
   });
@@ -845,7 +833,6 @@ int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
   return guard([&] {
     Engine& e = need(ge);
     std::shared_lock<std::shared_mutex> lk(e.mu);
-    same_part_snapshot(e);
     part_finish(e, d_out_perm, d_out_err);
   });
 }
