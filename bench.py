@@ -625,7 +625,10 @@ def main():
             **({"disagreements": disagree} if disagree else {}),
             "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),
                            "COND": int((res == 3).sum()), "ERR": int((errs != 0).sum())},
-            "engine": {"levels_per_bundle": round(st["levels"] / max(1, st["bundles"]), 2),
+            # levels: BFS levels run by the wave bundles (summed over bundles) plus the grid-wide
+            # and partitioned paths' levels; the closure join runs none
+            "engine": {"bfs_levels_per_batch": round(st["levels"] / n_batches, 2),
+                       "levels_per_bundle": round(st["levels"] / st["bundles"], 2) if st["bundles"] else None,
                        "bundles_per_batch": round(st["bundles"] / n_batches, 1),
                        "entries_per_batch": int(st["entries_expanded"] / n_batches),
                        "edges_per_batch": int(st["edges_enumerated"] / n_batches),

@@ -19,11 +19,11 @@ extern "C" {
 
 // Runs batches k = 0 .. n_batches-1 (device buffers items[k], perm[k], err[k], n checks each) with
 // up to `depth` in flight; batch k is submitted on streams[k % depth] with GCK_SUBMIT_DEVICE | flags
-// (GCK_SUBMIT_ENGINE_STREAM: on the engine's workspace streams instead). Returns GCK_OK or the first
+// (GCK_SUBMIT_ENGINE_STREAM: on the engine's workspace streams instead), at now_us (0 = the clock). Returns GCK_OK or the first
 // error; *seconds = wall time from the first submit to the last wait.
 int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs, size_t n_batches, const uint64_t* items,
              const uint64_t* perm, const uint64_t* err, size_t n, uint32_t depth, const uint64_t* streams,
-             uint32_t flags, double* seconds) {
+             uint32_t flags, int64_t now_us, double* seconds) {
   if (depth == 0) depth = 1;
   std::deque<gck_batch*> q;
   int rc = GCK_OK;
@@ -35,7 +35,7 @@ int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistenc
       if (rc != GCK_OK) break;
     }
     gck_batch* b = nullptr;
-    rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, 0,
+    rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, now_us,
                 reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), GCK_SUBMIT_DEVICE | flags,
                 reinterpret_cast<void*>(streams[k % depth]), &b);
     if (rc == GCK_OK) q.push_back(b);

@@ -213,7 +213,8 @@ def _driver():
         d = C.CDLL(path)
         d.gckd_run.restype = C.c_int
         d.gckd_run.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
-                               C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]
+                               C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int64,
+                               C.POINTER(C.c_double)]
         _DRIVER = d
     return _DRIVER
 
@@ -531,7 +532,8 @@ class Engine:
         """GCK_FLAG_PROFILE for the batches submitted from now on (gck_set_profile)."""
         _check(self._lib.gck_set_profile(self._h, 1 if on else 0))
 
-    def run_device_batches(self, items, perms, errs, n: int, depth: int, streams, engine_streams: bool = False) -> float:
+    def run_device_batches(self, items, perms, errs, n: int, depth: int, streams, engine_streams: bool = False,
+                           now_us: int = 0) -> float:
         """Checks len(items) device batches of n items each (device pointers items[k], perms[k],
         errs[k]) with up to `depth` in flight, batch k on streams[k % depth] (engine_streams: on
         the engine's workspace streams, GCK_SUBMIT_ENGINE_STREAM), through the compiled
@@ -545,7 +547,7 @@ class Engine:
         submit = C.cast(self._lib.gck_check_submit, C.c_void_p)
         wait = C.cast(self._lib.gck_check_wait, C.c_void_p)
         _check(drv.gckd_run(submit, wait, self._h, C.byref(cs), k, arr(items), arr(perms), arr(errs), n, depth,
-                            arr(streams), SUBMIT_ENGINE_STREAM if engine_streams else 0, C.byref(secs)))
+                            arr(streams), SUBMIT_ENGINE_STREAM if engine_streams else 0, now_us, C.byref(secs)))
         return secs.value
 
     # ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) --------

@@ -31,6 +31,14 @@ def test_library_exports_every_declared_symbol():
     assert sorted(E._SIGS) == declared
 
 
+def test_driver_library_exports_its_loop():
+    """bench.py's compiled submit/wait loop (csrc/driver.cpp) loads without a GPU."""
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(E.__file__), "libgck_driver.so")
+    assert hasattr(ctypes.CDLL(path), "gckd_run")
+
+
 def test_struct_layouts_match_header():
     assert E.ITEM_DTYPE.itemsize == 20
     assert E.TUPLE_DTYPE.itemsize == 32

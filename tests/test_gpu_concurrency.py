@@ -249,3 +249,29 @@ def test_pinned_host_buffers():
         e.submit_into(items.copy(), perm, err, now_us=gen.NOW_US).wait()
         assert _got(perm, err) == want
         e.close()
+
+
+@pytest.mark.parametrize("engine_streams", [False, True])
+def test_compiled_submit_loop(engine_streams):
+    """libgck_driver.so's loop (bench.py's timed region): 6 device batches, 3 in flight, on the
+    caller's streams or the engine's (GCK_SUBMIT_ENGINE_STREAM); every result equals the oracle."""
+    import torch
+    schema, tuples, checks = gen.github(4)
+    e = _engine(schema, tuples, workspaces=3)
+    want = _want(schema, tuples, checks)
+    items = e.make_items([parse_check(c) for c in checks])
+    n = len(items)
+    d_items = [torch.from_numpy(np.roll(items, k).view(np.uint8).copy()).cuda() for k in range(6)]
+    outs = [(torch.zeros(n, dtype=torch.uint8, device="cuda"), torch.zeros(n, dtype=torch.int32, device="cuda"))
+            for _ in range(6)]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    torch.cuda.synchronize()
+    secs = e.run_device_batches([d.data_ptr() for d in d_items], [p.data_ptr() for p, _ in outs],
+                                [x.data_ptr() for _, x in outs], n, 3, [streams[k % 3].cuda_stream for k in range(6)],
+                                engine_streams=engine_streams, now_us=gen.NOW_US)
+    torch.cuda.synchronize()
+    assert secs > 0
+    for k, (perm, err) in enumerate(outs):
+        rolled = (want[-k:] + want[:-k]) if k else want  # np.roll(items, k)[i] = items[i - k]
+        assert _got(perm.cpu().numpy(), err.cpu().numpy()) == rolled, k
+    e.close()
