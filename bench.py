@@ -260,7 +260,19 @@ def main():
         from gochugaru_amd.partition import PartitionedChecker, RcclPartitionedChecker
         # nccl: the level loop and its RCCL exchange inside libgck (gck_part_check); else the
         # Python driver over torch.distributed (gloo rehearsals)
-        pc = RcclPartitionedChecker(eng) if args.part_backend == "nccl" else PartitionedChecker(eng)
+        if args.part_backend == "nccl":
+            # RCCL prints its version banner on stdout when the communicator starts: keep stdout
+            # for the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                pc = RcclPartitionedChecker(eng)
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
+        else:
+            pc = PartitionedChecker(eng)
         items = torch.cat([WL.checks(args.batch, 1000 + r) for r in range(world)])
         n_global = args.batch * world
         out = {}

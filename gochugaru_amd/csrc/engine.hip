@@ -333,6 +333,11 @@ __device__ __forceinline__ int vinsert(const Ctx& c, unsigned long long key) {
 __device__ __forceinline__ uint32_t qflags(const DevQuery* q) {
   return __hip_atomic_load(&q->flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A query's flags read only to skip work for a decided query (a stale value costs an expansion
+// that the next level drops): no acquire, so no L1 invalidation (buffer_inv) per call.
+__device__ __forceinline__ uint32_t qflags_hint(const DevQuery* q) {
+  return __hip_atomic_load(&q->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void set_found(const Ctx& c, uint32_t q, uint32_t cond) {
   atomicOr(&c.queries[q].flags, (cond & kCondBit) ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
@@ -434,26 +439,30 @@ __device__ __forceinline__ bool visible(const DevCSR& r, uint32_t pos, int64_t n
 constexpr uint32_t kReqCap = 1u << 18;
 constexpr uint32_t kReqSet = 1u << 20;
 
-__device__ __noinline__ uint32_t cav_lazy(const Ctx& c, uint32_t row, uint32_t slot) {
+// (out of line — it is rare — with the Ctx fields it reads as arguments: a `const Ctx&` to an
+// out-of-line callee makes every thread of the calling kernel copy the whole Ctx to scratch)
+__device__ __noinline__ uint32_t cav_lazy(const unsigned long long* cav_keys, const uint8_t* cav_vals, uint64_t cav_kmask,
+                                          unsigned long long* req_set, unsigned long long* req_list, unsigned* req_cnt,
+                                          DevCounters* ctr, uint32_t row, uint32_t slot) {
   const unsigned long long key = ((unsigned long long)row << 32) | slot;
-  uint64_t h = mix64(key) & c.cav_kmask;
+  uint64_t h = mix64(key) & cav_kmask;
   for (int p = 0; p < 64; ++p) {  // the host keeps the map at most half full
-    const unsigned long long k = gptr(c.cav_keys)[h];
-    if (k == key) return gptr(c.cav_vals)[h];
+    const unsigned long long k = gptr(cav_keys)[h];
+    if (k == key) return gptr(cav_vals)[h];
     if (k == kEmptyKey) break;
-    h = (h + 1) & c.cav_kmask;
+    h = (h + 1) & cav_kmask;
   }
-  atomicAdd(&c.ctr->cav_requests, 1u);
-  if (__hip_atomic_load(c.req_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kReqCap) return 4u;
+  atomicAdd(&ctr->cav_requests, 1u);
+  if (__hip_atomic_load(req_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kReqCap) return 4u;
   uint64_t s = mix64(key) & (kReqSet - 1);
   for (int p = 0; p < 128; ++p) {
-    const unsigned long long v = __hip_atomic_load(&c.req_set[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long v = __hip_atomic_load(&req_set[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v == key) return 4u;
     if (v == kEmptyKey) {
-      const unsigned long long prev = atomicCAS(&c.req_set[s], kEmptyKey, key);
+      const unsigned long long prev = atomicCAS(&req_set[s], kEmptyKey, key);
       if (prev == kEmptyKey) {
-        const unsigned idx = atomicAdd(c.req_cnt, 1u);
-        if (idx < kReqCap) gptr_w(c.req_list)[idx] = key;
+        const unsigned idx = atomicAdd(req_cnt, 1u);
+        if (idx < kReqCap) gptr_w(req_list)[idx] = key;
         return 4u;
       }
       if (prev == key) return 4u;
@@ -473,7 +482,8 @@ __device__ __forceinline__ uint32_t cav_state(const Ctx& c, uint32_t cav, uint32
   const uint32_t slot = gptr(c.ck_items)[item].context_slot;
   if (slot == 0 || slot > c.n_ctx) return 2u;
   const uint32_t row = gptr(c.cav_row)[cav];
-  const uint32_t v = c.cav_keys ? cav_lazy(c, row, slot)
+  const uint32_t v = c.cav_keys ? cav_lazy(c.cav_keys, c.cav_vals, c.cav_kmask, c.req_set, c.req_list, c.req_cnt, c.ctr,
+                                          row, slot)
                                 : (uint32_t)gptr(c.cav_dyn)[(size_t)row * c.n_dist + gptr(c.cav_slot)[slot - 1]];
   if (v == 3u) {
     const uint32_t k = c.ck_map ? gptr(c.ck_map)[item] : c.ck_off + item;
@@ -593,7 +603,7 @@ __device__ __forceinline__ void emit_segment(const Ctx& c, uint32_t csr, uint32_
 // the entry's bits: the cond bit conditions the join's result (non-exact checks), the exact bit
 // passes on to the operands; an exact all() operand entered through a caveated tupleset edge is
 // tagged with the caveat's outcome (and_tag) instead of a cond bit.
-__device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth,
+__device__ __forceinline__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth,
                            uint32_t cond, uint32_t& rows) {
   const DevNode nd = c.nodes[node];
   const uint32_t check = c.queries[q].check;
@@ -691,7 +701,7 @@ __device__ void spawn_join(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node
 // false (kTagFalse) for this check: a single-operand join whose operand query walks from
 // (obj, node) and whose result reaches query q through and_tag. Deduplicated per (q, vertex,
 // depth, tag).
-__device__ void spawn_and(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth, uint32_t tag) {
+__device__ __forceinline__ void spawn_and(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node, uint32_t depth, uint32_t tag) {
   if (vinsert(c, make_key(c, q, node, tag, depth, obj)) <= 0) return;
   unsigned j = atomicAdd(&c.ctr->n_joins, 1u);
   unsigned q0 = atomicAdd(&c.ctr->n_queries, 1u);
@@ -788,7 +798,7 @@ __global__ void __launch_bounds__(kBlock) k_expand(Ctx c, const Entry* __restric
   if (i < n) {
     const Entry e = cur[i];
     DevQuery* q = &c.queries[e.q];
-    uint32_t qf = qflags(q);
+    uint32_t qf = qflags_hint(q);
     if (!(qf & QF_DONE)) {
       ++expanded;
       const DevCheck s = c.checks[q->check];
@@ -880,7 +890,7 @@ __global__ void __launch_bounds__(kBlock) k_edges(Ctx c) {
     const Segment s = c.segs[lo - 1];
     const unsigned long long off = eid - s.edge_start;
     if (off >= s.len) continue;  // a segment dropped on overflow
-    if (qflags(&c.queries[s.q]) & QF_DONE) continue;
+    if (qflags_hint(&c.queries[s.q]) & QF_DONE) continue;
     const DevCSR& r = c.csrs[s.csr];
     const uint32_t p = s.begin + (uint32_t)off;
     const uint32_t x = csr_nbr(r, p);
@@ -926,7 +936,7 @@ __device__ __forceinline__ bool try_finalize(DevQuery* q, uint32_t res) {
 }
 
 // Decide query `qi` with `res` and cascade the decision through its parent joins.
-__device__ void finalize(const Ctx& c, uint32_t qi, uint32_t res) {
+__device__ __forceinline__ void finalize(const Ctx& c, uint32_t qi, uint32_t res) {
   for (int guard = 0; guard < 1 << 20; ++guard) {
     DevQuery* q = &c.queries[qi];
     if (!try_finalize(q, res)) return;
