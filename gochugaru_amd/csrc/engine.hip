@@ -129,6 +129,7 @@ struct Workspace {
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
   bool b_closure = false;     // stage A began with the closure join: its leftovers are bundled in finish
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
+  bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
   unsigned b_seq = 0;         // publish sequence of stage A
   float b_ms = 0.f;
@@ -2558,6 +2559,7 @@ void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int
   stage_caveats(*w, std::move(cav), st);
   if (now_us == 0) now_us = wall_now_us();
   submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host);
+  w->b_own_stream = !host && engine_stream;
 }
 
 // Completes a submitted batch. Takes no engine lock: a writer that wants to replace the
@@ -2568,6 +2570,13 @@ void device_wait(Engine& e, Workspace* w) {
   std::lock_guard<std::mutex> lk(w->m);
   finish_batch(e, *w);  // no-op when a writer already finished it (drain_batches)
   w->state = 0;
+  // a device batch on the engine's stream: no caller stream orders its results, so the batch is
+  // complete — its kernels ended, their writes past the L2s — before the wait returns (the
+  // publication only says every block has decided)
+  if (w->b_own_stream) {
+    w->b_own_stream = false;
+    HIP_OK(hipStreamSynchronize(w->stream));
+  }
   if (w->fail_code) throw Error(w->fail_code, w->fail_msg);
   copy_out(*w);
   std::lock_guard<std::mutex> sl(e.stats_mu);
