@@ -1952,7 +1952,12 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
     j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
-    if (!host_out) {  // the join publishes the batch itself (a host batch's copies come first)
+    // the join publishes the batch itself, unless something must follow it first: a host batch's
+    // copies, or — for a device batch on the engine's stream, whose caller has no stream to order
+    // its reads — the join's end (k_publish after it sees every block's results written back
+    // past the L2s; the join's own last block sees only that every block has decided: a host-side
+    // stream query or synchronisation per batch instead costs ~10 us, 11 G -> 3-5 G checks/s)
+    if (!host_out && !w.b_own_stream) {
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
       j.h_out = w.d_hpub;
@@ -1983,7 +1988,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
-  if (!w.b_closure || host_out) publish_launch(w, st);
+  if (!w.b_closure || host_out || w.b_own_stream) publish_launch(w, st);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
@@ -2364,7 +2369,8 @@ void host_free_all(Engine& e) {
 }
 
 static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_t n, int64_t now_us, uint8_t* perm,
-                         int32_t* err, hipStream_t st, bool host) {
+                         int32_t* err, hipStream_t st, bool host, bool own_stream = false) {
+  w.b_own_stream = own_stream;
   w.b_n = n;
   w.b_now = now_us;
   w.b_st = host ? w.stream : st;
@@ -2558,8 +2564,7 @@ void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int
   hipStream_t st = (host || engine_stream) ? w->stream : (hipStream_t)stream;
   stage_caveats(*w, std::move(cav), st);
   if (now_us == 0) now_us = wall_now_us();
-  submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host);
-  w->b_own_stream = !host && engine_stream;
+  submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host, !host && engine_stream);
 }
 
 // Completes a submitted batch. Takes no engine lock: a writer that wants to replace the
@@ -2570,13 +2575,6 @@ void device_wait(Engine& e, Workspace* w) {
   std::lock_guard<std::mutex> lk(w->m);
   finish_batch(e, *w);  // no-op when a writer already finished it (drain_batches)
   w->state = 0;
-  // a device batch on the engine's stream: no caller stream orders its results, so the batch is
-  // complete — its kernels ended, their writes past the L2s — before the wait returns (the
-  // publication only says every block has decided)
-  if (w->b_own_stream) {
-    w->b_own_stream = false;
-    HIP_OK(hipStreamSynchronize(w->stream));
-  }
   if (w->fail_code) throw Error(w->fail_code, w->fail_msg);
   copy_out(*w);
   std::lock_guard<std::mutex> sl(e.stats_mu);

@@ -264,8 +264,10 @@ void device_lookup_subjects(Engine& e, Workspace& w, const gck_item& proto, int6
 // partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
 void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
 void part_expand(Engine& e, uint64_t* send_counts);
-void part_pack(Engine& e, void* d_send, size_t send_cap);
-void part_ingest(Engine& e, const void* d_recv, size_t n_recv, void* d_flags);
+// sync = false: the caller orders the next work on the partitioned batch's stream itself
+// (gck_part_check: RCCL on the same stream), so the step does not wait for its copies / kernels
+void part_pack(Engine& e, void* d_send, size_t send_cap, bool sync = true);
+void part_ingest(Engine& e, const void* d_recv, size_t n_recv, void* d_flags, bool sync = true);
 uint32_t part_resolve(Engine& e, const void* d_flags);
 void part_finish(Engine& e, uint8_t* d_perm, int32_t* d_err);
 void part_unique_id(uint8_t* out);
