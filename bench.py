@@ -35,7 +35,7 @@ BATCH = 65536
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # a 64K batch takes ~6 us of device time with 12 in flight: 2000 timed batches (~12 ms) keep
+    # a 64K batch takes ~6 us of device time with 8 in flight: 2000 timed batches (~12 ms) keep
     # the pipeline's fill and drain (a few batches' worth) and host jitter out of the figure
     # (configs 2, 3, 5: 200 / 20 — their steps are longer and config 5 pre-generates a Watch
     # batch or 64K contexts per step)
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="check batches in flight (gck_check_submit on this many streams): the next batch's "
-                         "kernels fill the tail of the previous one; 1 = one batch at a time (default: 16 for "
+                         "kernels fill the tail of the previous one; 1 = one batch at a time (default: 8 for "
                          "config 4, 3 for the others)")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
@@ -93,7 +93,7 @@ def parse():
     if args.warmup is None:
         args.warmup = 100 if nested else 20
     if args.inflight is None:
-        args.inflight = 16 if nested else 3
+        args.inflight = 8 if nested else 3
     return args
 
 
@@ -395,7 +395,7 @@ def main():
         eng.reset_stats()
         for k in range(min(len(rot), 48)):
             eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(), device=True,
-                       stream=streams[0].cuda_stream).wait()
+                       stream=streams[0].cuda_stream, engine_stream=bool(args.engine_streams)).wait()
         torch.cuda.synchronize()
         st_solo = eng.stats()
         eng.set_profile(False)
@@ -534,7 +534,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "kernel": ("k_closure_join (+ k_bundles<1> over what it leaves): stage A of a batch, timed by the "
                            "kernel's own start/stop HIP events (hipExtLaunchKernelGGL) on its launch stream, batches "
-                           "one at a time after the timed region; k_bundles<16> only for deferred giant checks"),
+                           "one at a time after the timed region, submitted as in the timed region (engine streams: "
+                           "k_publish follows the join); k_bundles<16> only for deferred giant checks"),
                 "alg_bytes_per_launch": int(b_alg),
                 # the whole job: algorithmic bytes of every timed batch / the timed region (launches
                 # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)
