@@ -4,17 +4,19 @@ Workload (BASELINE.json metric "permission checks/sec (whole node) at batch 64K,
 HBM GB/s vs peak"; config 4 of BASELINE.json configs, replicated-graph mode, which fits one
 MI355X): tests/synth.py builds the seeded graph on every rank (identical, replicated), the
 engine ingests it through the C ABI (gck_load_csr), and each step is one 65,536-item
-``doc#view@user`` batch per GPU through ``gck_check_bulk_device`` with the items already
-resident in HBM. Ranks check independent batches (no collective on the data path), so
-scaling is weak: value = (checks of all ranks) / (max-over-ranks time).
+``doc#view@user`` batch per GPU with the items already resident in HBM: 2,000 distinct
+pre-generated batches, 8 in flight (gck_check_submit / gck_check_wait on the engine's own
+streams, driven by the compiled loop of libgck_driver.so). Ranks check independent batches (no
+collective on the data path), so scaling is weak: value = (checks of all ranks) / (max-over-ranks
+time). Configs 2, 3, 5 (``--config``) run the same way with their own defaults.
 
-Also printed: the roofline of the dominant kernels (SURVEY.md §8d algorithmic bytes of the
-batch, counted by the oracle's counting mode, / the mean launch time of k_bundles<1> +
-k_bundles<16> from HIP events on the launch stream inside the timed region; `traffic` = HBM
-bytes per batch from rocprofv3 PMC, tools/pmc_traffic.sh -> profiles/r01/traffic.json) and a
-CPU baseline: the C restatement oracle (all 16 host threads) on a bounded sample — the timed
-batch plus further batches of the same generator, ~15 s of CPU work — with every sampled
-check compared against the GPU's answer (`oracle_agreement`).
+Also printed: the roofline of the dominant kernel (SURVEY.md §8d algorithmic bytes of a batch,
+counted by the oracle's counting mode, / the mean k_closure_join launch time from the kernel's
+own HIP events, batches one at a time after the timed region; `traffic` = HBM bytes per batch
+from rocprofv3 PMC, tools/pmc_r02.sh -> profiles/r02/traffic.json), the PCIe-inclusive rate over
+host buffers (never `value`), and a CPU baseline: the C restatement oracle (16 host threads) on a
+bounded sample of the same batches, ~15 s of CPU work, with every sampled check compared against
+the GPU's answer (`oracle_agreement`).
 """
 import argparse
 import collections
