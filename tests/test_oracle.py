@@ -129,3 +129,27 @@ def test_lookup_subjects_wildcard(case):
     st, _, srel = kind.partition("#")
     got = ck.lookup_subjects("doc", "d", perm, st, srel or ref.ELLIPSIS)
     assert sorted(got) == sorted(want)
+
+
+@pytest.mark.parametrize("family,seed", [("gdocs", 1), ("github", 2), ("nested", 3), ("caveated", 4)])
+def test_lookup_subjects_walk_matches_the_candidate_sweep(family, seed):
+    """The oracle's LookupSubjects walk against a brute-force sweep of every subject: the same
+    concrete subjects, except that the ones only a wildcard grants fold into "*" (and "*" is
+    reported exactly when an absent subject has the permission)."""
+    from tests import gen
+    schema, tuples, checks = gen.FAMILIES[family](seed)
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    users = sorted({t.split("@", 1)[1].split("[", 1)[0].split(":", 1)[1]
+                    for t in tuples if t.split("@", 1)[1].startswith("user:")} - {"*"})
+    for c in checks[:6]:
+        res = c.split("@", 1)[0]
+        rtype, rest = res.split(":", 1)
+        rid, perm = rest.split("#", 1)
+        got = dict(ck.lookup_subjects(rtype, rid, perm, "user"))
+        sweep = {u: p for u in users
+                 for p, err in [ck.check(ref.Item(rtype, rid, perm, "user", u))] if p in (ref.HAS, ref.COND)}
+        absent = ck.check(ref.Item(rtype, rid, perm, "user", "\x00absent"))[0]
+        assert ("*" in got) == (absent in (ref.HAS, ref.COND)), c
+        for u, p in sweep.items():
+            assert got.get(u) == p or ("*" in got and u not in got), (c, u)
+        assert all(u == "*" or u in sweep for u in got), c
