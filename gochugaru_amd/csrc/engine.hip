@@ -1967,10 +1967,15 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     }
     // a timed batch's events are the kernel's own start and stop (hipExtLaunchKernel), not markers
     // around its dispatch, so they agree with a profiler's kernel duration
-    const dim3 grid((n + 64u * kWaves - 1) / (64u * kWaves)), block(kBlock);
+    // GCK_CJ_CPW=32: 32 checks per wave (an A/B of the tail each wave waits for)
+    static const bool cpw32 = getenv("GCK_CJ_CPW") && atoi(getenv("GCK_CJ_CPW")) == 32;
+    const uint32_t cpw = cpw32 ? 32u : 64u;
+    const dim3 grid((n + cpw * kWaves - 1) / (cpw * kWaves)), block(kBlock);
     hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
     const bool small = j.table_bytes <= kCjLdsBytesSmall;
-    if (ds.slot_bits == 24 && small)
+    if (cpw32 && ds.slot_bits == 24 && small)
+      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32>), grid, block, 0, st, e0, e1, 0, c, j);
+    else if (ds.slot_bits == 24 && small)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
     else if (ds.slot_bits == 24)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytes>), grid, block, 0, st, e0, e1, 0, c, j);
