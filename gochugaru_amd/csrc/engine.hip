@@ -1968,7 +1968,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     // a timed batch's events are the kernel's own start and stop (hipExtLaunchKernel), not markers
     // around its dispatch, so they agree with a profiler's kernel duration
     // 32 checks per wave: each wave waits for the slowest of 64 lines instead of 128 (solo launch
-    // 12.1 vs 12.8 us, throughput +1 %, profiles/r02/sweep/cpw*); GCK_CJ_CPW=64 for the other
+    // 12.1-12.3 vs 12.8-12.9 us, the same throughput, profiles/r02/sweep/cpw*); GCK_CJ_CPW=64 for
+    // the other
     static const bool cpw32 = !(getenv("GCK_CJ_CPW") && atoi(getenv("GCK_CJ_CPW")) == 64);
     const uint32_t cpw = cpw32 ? 32u : 64u;
     const dim3 grid((n + cpw * kWaves - 1) / (cpw * kWaves)), block(kBlock);
