@@ -86,6 +86,7 @@ def parse():
                          "(tests/synth_configs.py) at --scale; mixed = config 5 (config 2 + 10 %% caveated "
                          "tuples, check contexts, one Watch batch of --churn x tuples applied per step); quota = "
                          "config 5 with 32K per-relationship caveat contexts x one context per request")
+    ap.add_argument("--selftest", action="store_true", help="launcher / rank bookkeeping only (no GPU; tests)")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     args = ap.parse_args()
@@ -96,6 +97,9 @@ def parse():
         args.warmup = 100 if nested else 20
     if args.inflight is None:
         args.inflight = 8 if nested else 3
+    # untimed batches before the timed region: at least --warmup, and at least two per batch in
+    # flight, so that every workspace, stream and hardware queue has run a batch before t0
+    args.warm = max(args.warmup, 2 * max(1, args.inflight))
     return args
 
 
@@ -202,6 +206,86 @@ class Workload:
                 loader(*c)
 
 
+def host_cpus():
+    """The host CPUs this process may use: its affinity mask, capped by a cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us) — nproc / os.cpu_count() report the
+    whole machine. Returns (usable, nproc)."""
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        usable = min(usable, max(1, int(quota)))
+    return usable, nproc
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU) with the
+    torch.distributed environment torchrun would give them, before this process touches a GPU,
+    and exit with the first failing rank's status. Rank 0's stdout (the JSON line) passes through."""
+    import socket
+    import subprocess
+    share = "--share-gpu" in sys.argv
+    if not share and "--selftest" not in sys.argv:
+        import torch  # counting devices does not initialise the GPU
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: only {have} GPU(s) visible; refusing to run fewer ranks",
+                  file=sys.stderr, flush=True)
+            sys.exit(2)
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+    if rc != 0:
+        print(f"bench.py --gpus {n}: a rank failed (status {rc})", file=sys.stderr, flush=True)
+    sys.exit(rc if rc > 0 else (1 if rc else 0))
+
+
+def selftest(args):
+    """The multi-rank bookkeeping without a GPU (tests/test_bench_launch.py): every rank joins the
+    gloo group, times a dummy step, and rank 0 prints the JSON line's rank-dependent keys."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    from gochugaru_amd.sharded import slices
+    b, e = slices(args.batch * world, world)[rank]
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "max_over_ranks": float(t[0]), "slice": [b, e],
+                          "global_batch": args.batch * world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def progress(msg):
     """Progress on stderr (long runs under a profiler must keep writing)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -209,6 +293,14 @@ def progress(msg):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args.gpus)  # does not return
+    if args.selftest:
+        return selftest(args)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world_env:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr, flush=True)
+        sys.exit(2)
     if args.hw_queues:  # before the HIP runtime starts
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
@@ -289,7 +381,7 @@ def main():
         perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
         err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
         n_up = max(1, int(n_tuples * args.churn))
-        batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warmup + args.steps)]
+        batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warm + args.steps)]
         rev = {"r": 1, "k": 0, "apply_s": 0.0}
 
         def step():
@@ -305,7 +397,7 @@ def main():
         # parsed, the walk records the (instance, context) pairs it meets, the host evaluates
         # them and the batch runs again — all inside the step
         from gochugaru_amd.engine import Contexts  # marshalled ahead, as the items are
-        q_rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(args.warmup + args.steps)]
+        q_rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(args.warm + args.steps)]
         q_rot = [(it, used, Contexts(texts)) for it, used, texts in q_rot]
         q_out = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
                   torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in q_rot]
@@ -322,7 +414,7 @@ def main():
         # distinct batches, rotated through warm-up and timed steps (no step re-reads a batch a
         # previous step left in the caches), each with its own result buffers; up to `depth`
         # of them in flight on as many streams (gck_check_submit / gck_check_wait)
-        n_rot = args.warmup + args.steps
+        n_rot = args.warm + args.steps
         rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(n_rot)]
         outs = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
                  torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
@@ -358,9 +450,9 @@ def main():
 
     native = run_steps is not None
     if native:
-        run_steps(args.warmup)
+        run_steps(args.warm)
     else:
-        for _ in range(args.warmup):
+        for _ in range(args.warm):
             step()
     if WL.kind not in ("mixed", "quota") and not args.partitioned:
         drain()
@@ -383,9 +475,9 @@ def main():
     elapsed = time.perf_counter() - t0
     progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms")
     if WL.kind not in ("mixed", "quota") and not args.partitioned:  # the first timed batch and its results
-        items, (perm, err) = rot[args.warmup], outs[args.warmup]
+        items, (perm, err) = rot[args.warm], outs[args.warm]
     if WL.kind == "quota":
-        items, (perm, err) = q_rot[args.warmup][0], q_out[args.warmup]
+        items, (perm, err) = q_rot[args.warm][0], q_out[args.warm]
     st = eng.stats()
     # per-launch time of the dominant kernel, alone on the GPU: the timed batches again, one at a
     # time, stage A timed by the kernel's own HIP events on its launch stream (every 4th batch of
@@ -424,9 +516,9 @@ def main():
     host_rate = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and args.host_steps > 0:
         # (up to 32 of the rotated batches, cycled: pinned host memory per batch is 1.6 MB)
-        n_h = min(len(rot), max(32, args.warmup + 1))
+        n_h = min(len(rot), max(32, args.warm + 1))
         h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot[:n_h]]
-        ref0 = (outs[args.warmup][0].cpu().numpy(), outs[args.warmup][1].cpu().numpy())
+        ref0 = (outs[args.warm][0].cpu().numpy(), outs[args.warm][1].cpu().numpy())
         # the same batches in pinned host memory (gck_host_alloc: DMA straight from / into them)
         p_rot = []
         for b in h_rot:
@@ -448,7 +540,7 @@ def main():
             return res
 
         def timed(dq, pinned):
-            host_run(args.warmup, dq, pinned)
+            host_run(args.warm, dq, pinned)
             t0 = time.perf_counter()
             r = host_run(args.host_steps, dq, pinned)
             dt = time.perf_counter() - t0
@@ -457,7 +549,7 @@ def main():
         hres, main = timed(depth, True)
         pres, pageable = timed(depth, False)
         _, one = timed(1, True)
-        k0 = args.warmup % len(h_rot)
+        k0 = args.warm % len(h_rot)
         same = all(k0 in r and (r[k0][0] == ref0[0]).all() and (r[k0][1] == ref0[1]).all() for r in (hres, pres))
         host_rate = {**main, "unit": "checks/s", "inflight": depth, "pageable": pageable, "one_at_a_time": one,
                      "same_results": bool(same),
@@ -467,34 +559,39 @@ def main():
 
     progress("host-buffer runs done")
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
+    # host threads for the oracle: the CPUs this process may use (affinity mask, cgroup quota),
+    # capped by OMP_NUM_THREADS when the box sets it (its per-GPU CPU share); nproc reports the
+    # whole machine
+    usable_cpus, nproc = host_cpus()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = args.cpu_threads or (min(usable_cpus, omp) if omp > 0 else usable_cpus)
+    cpu_note = (f"{threads} threads: sched_getaffinity/cgroup allow {usable_cpus} CPUs"
+                + (f", OMP_NUM_THREADS={omp}" if omp else "") + f", nproc {nproc}")
     prog = tab = None
     if rank == 0 and not args.no_oracle and WL.kind == "mixed":
         from oracle import corc  # the final snapshot (after every Watch batch) vs the timed batch
         hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
-        cp, ce = WL.M.expected(hi, threads=args.cpu_threads or min(16, os.cpu_count() or 1))
+        cp, ce = WL.M.expected(hi, threads=threads)
         agree_mixed = float(((cp == res) & (ce == errs)).mean())
     if rank == 0 and not args.no_oracle and WL.kind == "quota":
         from oracle import corc  # the first timed batch vs the C oracle's threshold mode
-        q_threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        q_threads = threads
         q_prog, q_tab, q_lim = WL.Q.oracle()
         hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
         t_q = time.perf_counter()
-        cp, ce = corc.check_quota(q_prog, q_tab, hi, q_lim, q_rot[args.warmup][1], threads=q_threads)
+        cp, ce = corc.check_quota(q_prog, q_tab, hi, q_lim, q_rot[args.warm][1], threads=q_threads)
         t_q = time.perf_counter() - t_q
         agree_mixed = float(((cp == res) & (ce == errs)).mean())
         if not args.no_cpu and world == 1:
             cpu_q = {"value": round(args.batch / t_q, 1), "unit": "checks/s", "cores": q_threads, "kind": "port",
                      "sample": f"the first timed batch ({args.batch} checks, {args.batch} contexts), C oracle "
                                f"threshold mode (oracle/check_oracle.c orc_check_quota: the caveat restated in C, "
-                               f"no CEL), OpenMP {q_threads} threads, {t_q:.2f}s"}
+                               f"no CEL), OpenMP {cpu_note}, {t_q:.2f}s"}
     if rank == 0 and not args.no_oracle and WL.kind not in ("mixed", "quota"):
         from oracle import corc
 
         prog, tab = WL.oracle()
         host_items = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
-    # host threads for the oracle: the box's CPU share (OMP_NUM_THREADS, 16 per GPU there) —
-    # nproc / os.cpu_count() report the whole host, which this process does not own
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
 
     # ---- roofline of the dominant kernels (SURVEY.md §8d algorithmic bytes) -------------------
     # One batch = stage A (k_closure_join over every check, then k_bundles<1> over what it left) and,
@@ -514,7 +611,7 @@ def main():
         n_cnt = min(4, args.steps) if WL.kind != "mixed" else 1
         cnt = collections.Counter()
         for k in range(n_cnt):
-            hk = (rot[args.warmup + k].cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+            hk = (rot[args.warm + k].cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
                   if WL.kind != "mixed" else host_items)
             if WL.union_only:
                 ck = corc.count_bfs(prog, tab, hk, threads=threads)
@@ -568,7 +665,7 @@ def main():
         per_batch = time.perf_counter() - t0
         extra = int(max(0, min(args.cpu_max_batches, args.cpu_seconds / max(per_batch, 1e-6))) - 1)
         # the timed batches with the results the timed region produced, then further batches
-        timed = list(range(args.warmup, args.warmup + args.steps)) if WL.kind != "mixed" else []
+        timed = list(range(args.warm, args.warm + args.steps)) if WL.kind != "mixed" else []
         batches = ([(rot[k], outs[k][0], outs[k][1]) for k in timed[:extra + 1]] if timed
                    else [(items, perm.clone(), err.clone())])
         extra = max(0, extra + 1 - len(batches))
@@ -604,8 +701,8 @@ def main():
         agree = n_ok / n_s
         cpu = {"value": round(n_s / dt, 1), "unit": "checks/s", "cores": threads, "kind": "port",
                "sample": f"{len(host)} batches x {args.batch} checks (the timed batches, then seeds 5000..), same "
-                         f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {threads} threads "
-                         f"= the box's CPU share; nproc reports {os.cpu_count()}), {dt:.1f}s; every sampled check "
+                         f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP "
+                         f"{cpu_note}), {dt:.1f}s; every sampled check "
                          f"compared with the GPU result"}
 
     progress("oracle / CPU baseline done")
@@ -623,15 +720,16 @@ def main():
             "metric": ("permission checks/sec (whole node) at batch 64K, 1B tuples" if WL.kind == "nested" else
                        f"permission checks/sec (whole node) at batch 64K, {WL.cfg['workload']}"),
             "value": round(value, 1), "unit": "checks/s", "n_gpus": 1 if args.share_gpu else world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "warmup_batches": args.warm, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": WL.data,
             "config": {**WL.cfg, "tuples": n_tuples, "batch_per_gpu": args.batch,
                        "parallelism": (f"graph partitioned x{world} by resource id, per-level all-to-all "
                                        f"({args.part_backend}), global batch {args.batch * world}")
                        if args.partitioned else
-                       (f"batch-sharded x{world} (rank r checks the r-th contiguous slice of a {args.batch * world}"
-                        f"-check request, gochugaru_amd/sharded.py), graph replicated, no data-path collective"
+                       (f"batch-sharded x{world}: one process per GPU, each rank checks its own stream of "
+                        f"{args.batch}-check batches against a full replica of the graph; no data-path collective "
+                        f"(barriers and the max-over-ranks time only)"
                         + (f", {world} ranks sharing one GPU" if args.share_gpu else "")),
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
             "roofline": roof, "cpu_baseline": cpu,
@@ -659,7 +757,7 @@ def main():
             **({"caveats": {"evals_per_step": round(st["caveat_evals"] / args.steps, 1),
                             "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}
                if WL.kind == "quota" else {}),
-            **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warmup + args.steps) * 1e3, 3),
+            **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warm + args.steps) * 1e3, 3),
                           "revision": rev["r"]}} if WL.kind == "mixed" else {}),
         }
         print(json.dumps(line), flush=True)

@@ -109,6 +109,7 @@ struct PartState;  // partition.inc
 struct Workspace {
   PartState* part = nullptr;  // partitioned batch in progress (partition.inc; Engine::part_ws only)
   bool busy = false;          // taken from the pool (Engine::ws_mu)
+  uint64_t bytes = 0;         // device scratch allocated for it (gck_device_bytes)
   size_t max_batch = 0, frontier_cap = 0, seg_cap = 0, query_cap = 0, join_cap = 0;
   uint64_t visited_cap = 0;
   // ---- the batch in flight (submit_batch .. finish_batch); guarded by `m` -----------------
@@ -1245,7 +1246,14 @@ void device_free(Engine& e) {
   }
 }
 
-uint64_t device_bytes(const Engine& e) { return e.dev ? e.dev->bytes : 0; }
+// The snapshot plus every workspace's scratch (gck_device_bytes).
+uint64_t device_bytes(Engine& e) {
+  uint64_t b = e.dev ? e.dev->bytes : 0;
+  std::lock_guard<std::mutex> lk(e.ws_mu);
+  for (const Workspace* w : e.ws_pool) b += w->bytes;
+  if (e.part_ws) b += e.part_ws->bytes;
+  return b;
+}
 
 // Host copies of the committed snapshot's own CSRs (not the derived indexes, which a load
 // rebuilds): the on-disk snapshot cache (snapfile.cpp) writes these.
@@ -1529,11 +1537,12 @@ static Workspace* create_workspace(Engine& e) {
     // the level / batch counters and the bundle counters share one buffer (one memset, one copy
     // back per batch)
     static_assert(sizeof(DevCounters) % 8 == 0, "bundle counters follow DevCounters");
-    w->ctr = reinterpret_cast<DevCounters*>(dalloc<unsigned char>(w->allocs, sizeof(DevCounters) + kBCtrs * sizeof(unsigned)));
+    w->ctr = reinterpret_cast<DevCounters*>(dalloc<unsigned char>(w->allocs, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), &w->bytes));
     w->b_ctrs = reinterpret_cast<unsigned*>(w->ctr + 1);
-    w->d_items = dalloc<gck_item>(w->allocs, w->max_batch);
-    w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
-    w->d_err = dalloc<int32_t>(w->allocs, w->max_batch);
+    w->d_items = dalloc<gck_item>(w->allocs, w->max_batch, &w->bytes);
+    w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch, &w->bytes);
+    w->d_err = dalloc<int32_t>(w->allocs, w->max_batch, &w->bytes);
+    w->cav_flag = dalloc<uint8_t>(w->allocs, w->max_batch, &w->bytes);
     HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters) + (kBCtrs + 4) * sizeof(unsigned),
                          hipHostMallocCoherent | hipHostMallocMapped));
     w->h_bctrs = reinterpret_cast<unsigned*>(w->h_ctr + 1);
@@ -1559,20 +1568,20 @@ static Workspace* create_workspace(Engine& e) {
       w->b_vslots = 1u << ceil_log2(cf.bundle_visited ? cf.bundle_visited : 16384);
       w->b_blocks = std::max<uint32_t>(1, cus * wpc / kWaves);
       const size_t slots = (size_t)w->b_blocks * kWaves;
-      w->b_fr = dalloc<unsigned long long>(w->allocs, slots * 2 * w->b_fc);
-      w->b_vis = dalloc<unsigned long long>(w->allocs, slots * w->b_vslots);
-      w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots);
+      w->b_fr = dalloc<unsigned long long>(w->allocs, slots * 2 * w->b_fc, &w->bytes);
+      w->b_vis = dalloc<unsigned long long>(w->allocs, slots * w->b_vslots, &w->bytes);
+      w->b_vlog = dalloc<uint32_t>(w->allocs, slots * w->b_vslots, &w->bytes);
       HIP_OK(hipMemsetAsync(w->b_vis, 0, slots * w->b_vslots * sizeof(unsigned long long), nullptr));
-      w->b_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
-      w->c_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
+      w->b_deferred = dalloc<uint32_t>(w->allocs, w->max_batch, &w->bytes);
+      w->c_deferred = dalloc<uint32_t>(w->allocs, w->max_batch, &w->bytes);
       w->b_budget = cf.bundle_budget ? cf.bundle_budget : 1024;
       w->g_fc = cf.giant_frontier ? cf.giant_frontier : 65536;
       w->g_vslots = 1u << ceil_log2(cf.giant_visited ? cf.giant_visited : 262144);
       w->g_slots = cf.giant_slots ? cf.giant_slots : cus;
-      w->g_deferred = dalloc<uint32_t>(w->allocs, w->max_batch);
-      w->def_items = dalloc<gck_item>(w->allocs, w->max_batch);
-      w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch);
-      w->def_err = dalloc<int32_t>(w->allocs, w->max_batch);
+      w->g_deferred = dalloc<uint32_t>(w->allocs, w->max_batch, &w->bytes);
+      w->def_items = dalloc<gck_item>(w->allocs, w->max_batch, &w->bytes);
+      w->def_perm = dalloc<uint8_t>(w->allocs, w->max_batch, &w->bytes);
+      w->def_err = dalloc<int32_t>(w->allocs, w->max_batch, &w->bytes);
     }
     HIP_OK(hipMemsetAsync(w->ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), nullptr));
     w->ctr_clean = true;
@@ -1592,14 +1601,14 @@ static Workspace* create_workspace(Engine& e) {
 // The grid-wide path's scratch (stage C, lookups' giant candidates, partitioned batches).
 static void ensure_wide(Workspace& w) {
   if (w.wide_ready) return;
-  w.checks = dalloc<DevCheck>(w.allocs, w.max_batch);
-  w.item_err = dalloc<int32_t>(w.allocs, w.max_batch);
-  w.queries = dalloc<DevQuery>(w.allocs, w.query_cap);
-  w.joins = dalloc<DevJoin>(w.allocs, w.join_cap);
-  w.fr[0] = dalloc<Entry>(w.allocs, w.frontier_cap);
-  w.fr[1] = dalloc<Entry>(w.allocs, w.frontier_cap);
-  w.segs = dalloc<Segment>(w.allocs, w.seg_cap);
-  w.visited = dalloc<unsigned long long>(w.allocs, w.visited_cap);
+  w.checks = dalloc<DevCheck>(w.allocs, w.max_batch, &w.bytes);
+  w.item_err = dalloc<int32_t>(w.allocs, w.max_batch, &w.bytes);
+  w.queries = dalloc<DevQuery>(w.allocs, w.query_cap, &w.bytes);
+  w.joins = dalloc<DevJoin>(w.allocs, w.join_cap, &w.bytes);
+  w.fr[0] = dalloc<Entry>(w.allocs, w.frontier_cap, &w.bytes);
+  w.fr[1] = dalloc<Entry>(w.allocs, w.frontier_cap, &w.bytes);
+  w.segs = dalloc<Segment>(w.allocs, w.seg_cap, &w.bytes);
+  w.visited = dalloc<unsigned long long>(w.allocs, w.visited_cap, &w.bytes);
   HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
   w.wide_ready = true;
 }
@@ -1607,9 +1616,9 @@ static void ensure_wide(Workspace& w) {
 // The workgroup-bundle stage's scratch (stage B).
 static void ensure_giant(Workspace& w) {
   if (w.giant_ready) return;
-  w.g_fr = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * 2 * w.g_fc);
-  w.g_vis = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * w.g_vslots);
-  w.g_vlog = dalloc<uint32_t>(w.allocs, (size_t)w.g_slots * w.g_vslots);
+  w.g_fr = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * 2 * w.g_fc, &w.bytes);
+  w.g_vis = dalloc<unsigned long long>(w.allocs, (size_t)w.g_slots * w.g_vslots, &w.bytes);
+  w.g_vlog = dalloc<uint32_t>(w.allocs, (size_t)w.g_slots * w.g_vslots, &w.bytes);
   HIP_OK(hipMemsetAsync(w.g_vis, 0, (size_t)w.g_slots * w.g_vslots * sizeof(unsigned long long), nullptr));
   HIP_OK(hipStreamSynchronize(nullptr));
   w.giant_ready = true;
@@ -1618,23 +1627,50 @@ static void ensure_giant(Workspace& w) {
 // A free workspace of the pool (created while the pool holds fewer than cfg.workspaces;
 // otherwise waits for one to be released). Call without holding the engine lock: the holders of
 // busy workspaces may need it to finish their batches.
-Workspace* acquire_ws(Engine& e) {
-  const size_t cap = e.cfg.workspaces ? e.cfg.workspaces : 4;
+static size_t pool_cap(const Engine& e) { return e.cfg.workspaces ? e.cfg.workspaces : 4; }
+
+// Every workspace of the pool, created up front (gck_commit_snapshot / gck_load_snapshot_file):
+// a check never pays for creating one (~0.5 GB of scratch, pinned staging, a stream and its
+// events, a synchronisation of the null stream) — the first `workspaces` concurrent batches
+// would otherwise each pay it inside the caller's latency.
+void ensure_pool(Engine& e) {
+  if (e.part_world > 1) return;  // a partitioned engine runs on its own workspace (part_ws)
+  std::lock_guard<std::mutex> lk(e.ws_mu);
+  while (e.ws_pool.size() < pool_cap(e)) e.ws_pool.push_back(create_workspace(e));
+}
+
+// `want` (1 or 2) free workspaces of the pool, taken together: a caller never holds one while it
+// waits for another (two callers each holding one and waiting for a second would deadlock a
+// pool of two, and one caller would deadlock a pool of one). A pool of one serves `want` = 2
+// with its single workspace (out[1] = out[0]). Workspaces missing from the pool (before
+// ensure_pool) are created here. Call without holding the engine lock: the holders of busy
+// workspaces may need it to finish their batches.
+void acquire_ws_n(Engine& e, int want, Workspace** out) {
+  const size_t cap = pool_cap(e);
+  const size_t need = std::min<size_t>((size_t)want, cap);
   std::unique_lock<std::mutex> lk(e.ws_mu);
   for (;;) {
+    std::vector<Workspace*> got;
     for (Workspace* w : e.ws_pool)
-      if (!w->busy) {
-        w->busy = true;
-        return w;
-      }
-    if (e.ws_pool.size() < cap) {
+      if (!w->busy && got.size() < need) got.push_back(w);
+    while (got.size() < need && e.ws_pool.size() < cap) {
       Workspace* w = create_workspace(e);
-      w->busy = true;
       e.ws_pool.push_back(w);
-      return w;
+      got.push_back(w);
+    }
+    if (got.size() == need) {
+      for (Workspace* w : got) w->busy = true;
+      for (int k = 0; k < want; ++k) out[k] = got[std::min<size_t>((size_t)k, need - 1)];
+      return;
     }
     e.ws_cv.wait(lk);
   }
+}
+
+Workspace* acquire_ws(Engine& e) {
+  Workspace* w = nullptr;
+  acquire_ws_n(e, 1, &w);
+  return w;
 }
 
 void release_ws(Engine& e, Workspace* w) {
@@ -1642,7 +1678,7 @@ void release_ws(Engine& e, Workspace* w) {
     std::lock_guard<std::mutex> lk(e.ws_mu);
     w->busy = false;
   }
-  e.ws_cv.notify_one();
+  e.ws_cv.notify_all();  // a two-workspace caller may be waiting beside one-workspace callers
 }
 
 static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
@@ -2203,10 +2239,12 @@ static void grow(Workspace& w, T*& p, size_t& cap, size_t want) {
     w.allocs.erase(std::remove(w.allocs.begin(), w.allocs.end(), (void*)p), w.allocs.end());
     HIP_OK(hipFree(p));
     p = nullptr;
+    w.bytes -= cap * sizeof(T);
   }
   cap = std::max(want, cap * 2);
   HIP_OK(hipMalloc(&p, cap * sizeof(T)));
   w.allocs.push_back(p);
+  w.bytes += cap * sizeof(T);
 }
 
 // Uploads the lazy map: every pair evaluated so far, open addressing at most half full.
@@ -2243,10 +2281,6 @@ static void stage_caveats(Workspace& w, CavCall&& call, hipStream_t st) {
   w.cav_eval.clear();
   w.cav_parsed.clear();
   if (!w.cav_on) return;
-  if (!w.cav_flag) {
-    HIP_OK(hipMalloc(&w.cav_flag, std::max<size_t>(w.max_batch, 1)));
-    w.allocs.push_back(w.cav_flag);
-  }
   if (!w.cav_lazy) {
     grow(w, w.cav_dyn, w.cav_dyn_cap, w.cav.dense.size());
     grow(w, w.cav_slot, w.cav_slot_cap, w.cav.of_slot.size());
@@ -2257,9 +2291,9 @@ static void stage_caveats(Workspace& w, CavCall&& call, hipStream_t st) {
     return;
   }
   if (!w.req_set) {
-    w.req_set = dalloc<unsigned long long>(w.allocs, kReqSet);
-    w.req_list = dalloc<unsigned long long>(w.allocs, kReqCap);
-    w.req_cnt = dalloc<unsigned>(w.allocs, 1);
+    w.req_set = dalloc<unsigned long long>(w.allocs, kReqSet, &w.bytes);
+    w.req_list = dalloc<unsigned long long>(w.allocs, kReqCap, &w.bytes);
+    w.req_cnt = dalloc<unsigned>(w.allocs, 1, &w.bytes);
     HIP_OK(hipStreamSynchronize(nullptr));  // the allocations are ordered on the null stream
   }
   HIP_OK(hipMemsetAsync(w.req_set, 0xFF, (size_t)kReqSet * 8, st));

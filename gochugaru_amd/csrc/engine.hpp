@@ -224,7 +224,9 @@ void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
 // a free one. Callers take their workspaces BEFORE the engine lock (the holders of busy ones
 // may need the lock to finish their batches).
 Workspace* acquire_ws(Engine& e);
+void acquire_ws_n(Engine& e, int want, Workspace** out);  // 1 or 2 together (no hold-and-wait)
 void release_ws(Engine& e, Workspace* w);
+void ensure_pool(Engine& e);  // every workspace of the pool, created after a snapshot commit
 struct WsLease {
   Engine& e;
   Workspace* w;
@@ -253,7 +255,7 @@ void host_free_all(Engine& e);
 // Finishes every batch in flight (a writer holding the engine exclusively calls this before
 // it replaces the snapshot: the batches keep the results of the snapshot they started on).
 void drain_batches(Engine& e);
-uint64_t device_bytes(const Engine& e);
+uint64_t device_bytes(Engine& e);
 void device_export(Engine& e, std::vector<HostCSR>& out);
 // lookups (lookup.inc): candidates [0, n) of the varying id of `proto` (resource id when
 // vary_res, else subject id); matching ids ascending with their permissionship

@@ -421,6 +421,7 @@ int gck_commit_snapshot(gck_engine* ge) {
     drain_batches(e);
     std::vector<HostCSR> csrs = build_csrs(e);
     device_upload(e, csrs);  // device-pointer CSRs are copied before the caller regains control
+    ensure_pool(e);          // no check ever creates a workspace (engine.hip ensure_pool)
     e.staged.clear();
     e.staged.shrink_to_fit();
     e.staging = false;
@@ -446,6 +447,7 @@ int gck_load_snapshot_file(gck_engine* ge, const char* path) {
     std::unique_lock<std::shared_mutex> lk(e.mu);
     drain_batches(e);
     load_snapshot_file(e, path);
+    ensure_pool(e);
   });
 }
 
@@ -649,14 +651,23 @@ int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item
     }
     // workspaces first, then the engine lock (engine.hpp WsLease)
     precheck(e);
+    // a request above max_batch alternates over two workspaces, taken in one step (never one
+    // held while waiting for the other: acquire_ws_n)
     const size_t mb = e.cfg.max_batch ? e.cfg.max_batch : 65536;
-    WsLease l0(e);
-    std::unique_ptr<WsLease> l1;
-    if (n > mb) l1.reset(new WsLease(e));
+    Workspace* ws[2] = {nullptr, nullptr};
+    acquire_ws_n(e, n > mb ? 2 : 1, ws);
+    struct Release {
+      Engine& e;
+      Workspace** ws;
+      ~Release() {
+        release_ws(e, ws[0]);
+        if (ws[1] && ws[1] != ws[0]) release_ws(e, ws[1]);
+      }
+    } rel{e, ws};
     std::shared_lock<std::shared_mutex> lk(e.mu);
     check_request(e, cs, items, n, true, contexts, context_lens, n_contexts);
     const CavCall cav = caveat_call(e, contexts, context_lens, n_contexts);
-    device_check_host(e, l0.w, l1 ? l1->w : nullptr, items, n, now_us, out_perm, out_err, cav);
+    device_check_host(e, ws[0], ws[1], items, n, now_us, out_perm, out_err, cav);
   });
 }
 

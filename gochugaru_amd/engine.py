@@ -11,6 +11,7 @@ import ctypes as C
 import json
 import os
 import time
+import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -280,14 +281,27 @@ class Engine:
         _check(lib.gck_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self._lib = lib
+        self._pins = 0          # live host_array() buffers (each keeps the engine handle alive)
+        self._closing = False
         self._type_ids = {}
         self._rel_ids = {}
         self.part_rank, self.part_world = 0, 1
 
     def close(self):
-        if self._h:
+        """Destroys the engine — once the last host_array() buffer is gone, since gck_destroy
+        frees the pinned memory those arrays view."""
+        self._closing = True
+        if self._h and self._pins == 0:
             self._lib.gck_destroy(self._h)
             self._h = None
+
+    def _unpin(self, p):
+        self._pins -= 1
+        if self._h:
+            self._lib.gck_host_free(self._h, p)
+            if self._closing and self._pins == 0:
+                self._lib.gck_destroy(self._h)
+                self._h = None
 
     def __del__(self):
         try:
@@ -507,18 +521,26 @@ class Engine:
 
     def host_array(self, n: int, dtype) -> np.ndarray:
         """A numpy array in pinned host memory (gck_host_alloc): host batches over such arrays
-        are copied by DMA directly. Freed with the engine."""
+        are copied by DMA directly. The memory is returned (gck_host_free) when the array and
+        every view of it are gone; the engine itself stays alive until then, even past close().
+        A batch submitted over it reads the items by DMA until its wait (include/gck.h)."""
+        if not self._h or self._closing:
+            raise GckError(GCK_E_STATE, "engine closed")
         dtype = np.dtype(dtype)
         p = _P()
         _check(self._lib.gck_host_alloc(self._h, max(1, n * dtype.itemsize), C.byref(p)))
         buf = (C.c_char * max(1, n * dtype.itemsize)).from_address(p.value)
+        self._pins += 1
+        weakref.finalize(buf, self._unpin, p.value)  # numpy views keep `buf` alive
         return np.frombuffer(buf, dtype=dtype, count=n)
 
     def submit_into(self, items: np.ndarray, perm: np.ndarray, err: np.ndarray,
                     requirement: int = CONSISTENCY_MIN_LATENCY, revision: int = 0, now_us: int = 0,
                     contexts: Optional[Sequence] = None) -> "Batch":
         """A host batch writing its results into caller-provided arrays (pinned ones from
-        host_array() skip the engine's staging copies)."""
+        host_array() skip the engine's staging copies). Items in a host_array() buffer are read by
+        DMA while the batch runs: leave them unchanged until wait() returns (include/gck.h
+        gck_check_submit); other host items are staged before this returns."""
         cs = _Consistency(requirement, 0, revision)
         ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
         h = _P()

@@ -16,6 +16,7 @@ order (the order ``Client.Check`` maps them in, client/client.go:271-283):
 """
 from __future__ import annotations
 
+from collections import deque
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -43,7 +44,10 @@ class ShardedEngine:
             raise ValueError("at least one device")
         self.devices = list(devices)
         self.engines = [Engine(device=d, **engine_kw) for d in self.devices]
-        self.max_batch = engine_kw.get("max_batch", 65536)
+        self.max_batch = engine_kw.get("max_batch") or 65536  # 0 = the engine's default
+        # batches one replica may have in flight: its workspace pool (gck_config.workspaces,
+        # 0 = 4). A submit beyond it would wait for a workspace its own caller holds.
+        self.depth = engine_kw.get("workspaces") or 4
 
     def close(self):
         for e in self.engines:
@@ -88,7 +92,10 @@ class ShardedEngine:
     def check_bulk(self, items: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY, revision: int = 0,
                    now_us: int = 0, contexts: Optional[Sequence] = None) -> Tuple[np.ndarray, np.ndarray]:
         """One request over all replicas: slice k (contiguous) on replica k, in chunks of
-        max_batch submitted before anything is waited for; results in request order."""
+        max_batch. Chunks are submitted round-robin over the replicas with at most `depth` in
+        flight per replica (the oldest of a replica is waited for before its next submit: never
+        more outstanding batches than its workspace pool, include/gck.h); results in request
+        order."""
         items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
         n = len(items)
         perm = np.zeros(n, dtype=np.uint8)
@@ -96,16 +103,36 @@ class ShardedEngine:
         if n == 0:
             self.engines[0].check_bulk(items, requirement, revision, now_us, contexts)  # consistency errors
             return perm, err
-        pending = []
-        for e, (b, en) in zip(self.engines, slices(n, len(self.engines))):
-            for c in range(b, en, self.max_batch):
-                ce = min(en, c + self.max_batch)
-                pending.append((c, ce, e.submit(items[c:ce], requirement=requirement, revision=revision,
-                                                now_us=now_us, contexts=contexts)))
-        for c, ce, bt in pending:
+        chunks = [[(c, min(en, c + self.max_batch)) for c in range(b, en, self.max_batch)]
+                  for b, en in slices(n, len(self.engines))]
+        inflight = [deque() for _ in self.engines]
+
+        def finish(q):
+            c, ce, bt = q.popleft()
             p, x = bt.wait()
             perm[c:ce] = p
             err[c:ce] = x
+
+        try:
+            for k in range(max(len(ch) for ch in chunks)):
+                for r, e in enumerate(self.engines):
+                    if k >= len(chunks[r]):
+                        continue
+                    if len(inflight[r]) >= self.depth:
+                        finish(inflight[r])
+                    c, ce = chunks[r][k]
+                    inflight[r].append((c, ce, e.submit(items[c:ce], requirement=requirement, revision=revision,
+                                                        now_us=now_us, contexts=contexts)))
+            for q in inflight:
+                while q:
+                    finish(q)
+        finally:  # an error leaves no batch holding a workspace
+            for q in inflight:
+                for _, _, bt in q:
+                    try:
+                        bt.wait()
+                    except Exception:
+                        pass
         return perm, err
 
 
@@ -131,15 +158,21 @@ class DistributedChecker:
         return self.checker.check_bulk(items[b:e], **kw)
 
     def gather(self, n: int, perm: np.ndarray, err: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """Every rank's slice, in request order, on every rank (gloo: host tensors; nccl/RCCL:
+        the rank's current GPU, which that backend requires)."""
         import torch
         parts = slices(n, self.world)
         width = max(e - b for b, e in parts)
+        dev = (torch.device("cuda", torch.cuda.current_device())
+               if self.dist.get_backend(self.group) == "nccl" else torch.device("cpu"))
         buf = torch.zeros(width, 5, dtype=torch.uint8)
         k = len(perm)
         buf[:k, 0] = torch.from_numpy(perm)
         buf[:k, 1:] = torch.from_numpy(err.astype(np.int32).view(np.uint8).reshape(k, 4))
+        buf = buf.to(dev)
         out = [torch.zeros_like(buf) for _ in range(self.world)]
         self.dist.all_gather(out, buf, group=self.group)
+        out = [t.cpu() for t in out]
         perm_all = np.zeros(n, dtype=np.uint8)
         err_all = np.zeros(n, dtype=np.int32)
         for (b, e), t in zip(parts, out):

@@ -39,7 +39,8 @@
  *
  * Ownership: all inputs and outputs are caller-allocated; the engine never retains a caller
  * pointer after a call returns, except that gck_check_submit keeps the output pointers (and, for
- * device batches, the item pointer) until the matching gck_check_wait. Return value: GCK_OK (0)
+ * device batches or host items in gck_host_alloc memory, the item pointer) until the matching
+ * gck_check_wait. Return value: GCK_OK (0)
  * or a negative GCK_E_* status; the message is available from gck_last_error() (thread-local).
  * Threading: gck_check_bulk*, gck_check_submit / gck_check_wait and the lookups may be called
  * concurrently from any number of threads: each batch in flight runs on its own pooled
@@ -329,8 +330,9 @@ int gck_check_bulk_device_ctx(gck_engine* e, const gck_item* d_items, size_t n,
  * once with a handle; gck_check_wait(handle) completes it (results written, handle consumed).
  * Every submitted batch must be waited for exactly once. GCK_SUBMIT_DEVICE: items / out_perm /
  * out_err are device buffers ordered on `stream` (as gck_check_bulk_device_ctx); otherwise they
- * are host buffers (the items are staged before the call returns; the outputs are written by the
- * wait). Consistency is checked at submit; the batch sees the snapshot current at submit, even if
+ * are host buffers (the outputs are written by the wait; pageable items are staged before the
+ * call returns, while items in gck_host_alloc memory are read by DMA as the batch runs and must
+ * stay unchanged until gck_check_wait returns). Consistency is checked at submit; the batch sees the snapshot current at submit, even if
  * a Watch batch is applied before the wait. GCK_SUBMIT_DEVICE | GCK_SUBMIT_ENGINE_STREAM: device
  * buffers, but the batch runs on the stream of the workspace it holds (created by the engine, one
  * per workspace, so that batches in flight sit on distinct hardware queues) and `stream` is
@@ -346,7 +348,8 @@ int gck_check_submit(gck_engine* e, const gck_consistency* cs, const gck_item* i
 int gck_check_wait(gck_engine* e, gck_batch* batch);
 /* Pinned host memory for request / result buffers: a host batch (gck_check_bulk*,
  * gck_check_submit) whose items or results lie in such a buffer is copied over PCIe by DMA
- * directly, skipping the engine's own staging copy. Freed with gck_host_free (or gck_destroy). */
+ * directly, skipping the engine's own staging copy (a submitted batch then reads its items there
+ * until gck_check_wait). Freed with gck_host_free (or gck_destroy). */
 int gck_host_alloc(gck_engine* e, size_t bytes, void** out);
 int gck_host_free(gck_engine* e, void* p);
 int gck_last_stats(gck_engine* e, gck_stats* out);

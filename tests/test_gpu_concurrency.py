@@ -275,3 +275,72 @@ def test_compiled_submit_loop(engine_streams):
         rolled = (want[-k:] + want[:-k]) if k else want  # np.roll(items, k)[i] = items[i - k]
         assert _got(perm.cpu().numpy(), err.cpu().numpy()) == rolled, k
     e.close()
+
+
+def test_no_allocation_after_commit():
+    """Every workspace exists once the snapshot is committed (engine.hip ensure_pool): the first
+    batches after the commit — as many concurrent ones as the pool holds — allocate nothing, so
+    no caller's latency includes creating a workspace. gck_device_bytes counts the snapshot plus
+    every workspace's scratch."""
+    schema, tuples, checks = gen.nested(2)
+    e = _engine(schema, tuples, workspaces=4)
+    want = _want(schema, tuples, checks)
+    items = e.make_items([parse_check(c) for c in checks])
+    before = e.device_bytes
+    assert before > 4 * 64 << 20, before  # four workspaces' bundle scratch is in the count
+    bs = [e.submit(items, now_us=gen.NOW_US) for _ in range(4)]  # the whole pool at once
+    for b in bs:
+        perm, err = b.wait()
+        assert _got(perm, err) == want
+    perm, err = e.check_bulk(items, now_us=gen.NOW_US)
+    assert _got(perm, err) == want
+    assert e.device_bytes == before
+    e.close()
+
+
+def test_two_workspace_requests_never_deadlock():
+    """A request above max_batch alternates over two workspaces, taken together
+    (gck_api.cpp gck_check_bulk_ctx / acquire_ws_n): with one workspace it runs on that one, and
+    four threads sending such requests to a pool of two all finish."""
+    schema, tuples, checks = gen.gdocs(6)
+    want = _want(schema, tuples, checks)
+    reps = 12
+    for ws, n_threads in ((1, 1), (1, 3), (2, 4)):
+        e = _engine(schema, tuples, workspaces=ws, max_batch=256)
+        items = e.make_items([parse_check(c) for c in checks] * reps)
+        assert len(items) > 2 * 256
+        errors, done = [], []
+
+        def worker():
+            try:
+                for _ in range(3):
+                    perm, err = e.check_bulk(items, now_us=gen.NOW_US)
+                    assert _got(perm, err) == want * reps
+                done.append(1)
+            except Exception as ex:  # noqa: BLE001
+                errors.append(ex)
+
+        threads = [threading.Thread(target=worker) for _ in range(n_threads)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=90)
+        assert not errors, errors
+        assert len(done) == n_threads, f"workspaces={ws}: {n_threads - len(done)} callers stuck"
+        e.close()
+
+
+def test_pinned_array_outlives_close():
+    """host_array() memory stays valid after Engine.close() while an array views it (the engine is
+    destroyed with its last pinned buffer)."""
+    schema, tuples, checks = gen.nested(1)
+    e = _engine(schema, tuples)
+    a = e.host_array(1000, np.int32)
+    a[:] = np.arange(1000)
+    e.close()
+    assert e._h is not None  # kept for `a`
+    assert int(a.sum()) == 499500
+    del a
+    import gc
+    gc.collect()
+    assert e._h is None

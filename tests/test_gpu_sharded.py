@@ -40,3 +40,23 @@ def test_sharded_equals_single_engine_and_oracle(replicas):
     assert np.array_equal(p12, perm2) and np.array_equal(e12, err2)
     one.close()
     se.close()
+
+
+def test_sharded_bounds_batches_in_flight():
+    """A slice of more chunks than a replica's workspace pool: the sharded engine waits for a
+    replica's oldest batch before its next submit (never more outstanding batches than
+    workspaces, include/gck.h), so the request completes; max_batch=0 means the default."""
+    schema, tuples, checks = gen.gdocs(4)
+    checks = checks * 30
+    se = ShardedEngine([0, 0], max_batch=256, workspaces=2)  # 6,000 checks per slice = 24 chunks
+    se.load_schema(schema)
+    se.load_snapshot_text(1, "\n".join(tuples))
+    items = se.make_items([parse_check(c) for c in checks])
+    perm, err = se.check_bulk(items, now_us=gen.NOW_US)
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks[:400]]
+    assert all((int(perm[i]), int(err[i])) == want[i % 400] for i in range(len(checks)))
+    se.close()
+    se0 = ShardedEngine([0], max_batch=0)
+    assert se0.max_batch == 65536
+    se0.close()
