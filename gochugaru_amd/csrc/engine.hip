@@ -2578,6 +2578,13 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
     Workspace& w = *ws[k & 1];
     const size_t pos = k * mb;
     const uint32_t len = (uint32_t)std::min(n - pos, mb);
+    if (prev == &w) {  // one workspace (a pool of one): the previous chunk completes first
+      finish_batch(e, w);
+      copy_out(w);
+      w.state = 0;
+      ms += w.b_ms;
+      prev = nullptr;
+    }
     submit_batch(e, w, items + pos, len, now_us, perm + pos, err + pos, nullptr, true);
     if (prev) {
       finish_batch(e, *prev);
