@@ -438,15 +438,27 @@ def main():
 
         if args.driver == "native":
             # the same submit/wait loop, run by the compiled caller (libgck_driver.so) over the
-            # steps of one phase: run_steps(count) checks the next `count` rotated batches
-            def run_steps(count):
-                k0 = cursor["k"]
-                cursor["k"] += count
+            # steps of one phase: run_steps(count) checks the next `count` rotated batches; the
+            # loop's arguments are marshalled before the phase (prepare), so a timed phase is the C
+            # loop alone
+            prepared = {}
+
+            def prepare(count):
+                k0 = cursor["k"] + sum(c for c, _ in prepared.values())
                 ks = range(k0, k0 + count)
-                eng.run_device_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
-                                       [outs[k][1].data_ptr() for k in ks], args.batch, depth,
-                                       [streams[(k - k0) % depth].cuda_stream for k in ks],
-                                       engine_streams=bool(args.engine_streams))
+                prepared[len(prepared)] = (count, eng.prepare_batches(
+                    [rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
+                    [outs[k][1].data_ptr() for k in ks], args.batch, depth,
+                    [streams[(k - k0) % depth].cuda_stream for k in ks], engine_streams=bool(args.engine_streams)))
+
+            def run_steps(count):
+                c, run = prepared.pop(min(prepared))
+                assert c == count
+                cursor["k"] += count
+                run.run()
+
+            prepare(args.warm)
+            prepare(args.steps)
 
     native = run_steps is not None
     if native:
@@ -546,16 +558,36 @@ def main():
             dt = time.perf_counter() - t0
             return r, {"value": round(args.host_steps * args.batch / dt, 1),
                        "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
-        hres, main = timed(depth, True)
+
+        def timed_native(dq):
+            # the compiled loop (libgck_driver.so gckd_run_host) over the pinned batches, cycled
+            ks = [j % len(p_rot) for j in range(args.host_steps)]
+            wk = [j % len(p_rot) for j in range(args.warm)]
+            mk = lambda kk: eng.prepare_batches([p_rot[k][0].ctypes.data for k in kk], [p_rot[k][1].ctypes.data for k in kk],
+                                                [p_rot[k][2].ctypes.data for k in kk], args.batch, dq, host=True)
+            warm_run, run = mk(wk), mk(ks)
+            warm_run.run()
+            dt = run.run()
+            k0_ = ks[-1]
+            return {k0_: (p_rot[k0_][1].copy(), p_rot[k0_][2].copy())}, {
+                "value": round(args.host_steps * args.batch / dt, 1), "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
+        nres, main = timed_native(depth)
+        hres, py_pinned = timed(depth, True)
         pres, pageable = timed(depth, False)
         _, one = timed(1, True)
         k0 = args.warm % len(h_rot)
+        kn = (args.host_steps - 1) % len(p_rot)
+        refn = (outs[kn][0].cpu().numpy(), outs[kn][1].cpu().numpy())
         same = all(k0 in r and (r[k0][0] == ref0[0]).all() and (r[k0][1] == ref0[1]).all() for r in (hres, pres))
-        host_rate = {**main, "unit": "checks/s", "inflight": depth, "pageable": pageable, "one_at_a_time": one,
+        same = same and all((nres[kn][j] == refn[j]).all() for j in (0, 1))
+        host_rate = {**main, "unit": "checks/s", "inflight": depth, "driver": "native",
+                     "python_pinned": py_pinned, "pageable": pageable, "one_at_a_time": one,
                      "same_results": bool(same),
-                     "note": "gck_check_submit/wait over host buffers, rotated batches: 20-B items H2D by DMA from "
-                             "pinned host memory (gck_host_alloc), kernels, 1+4 B results D2H into pinned host "
-                             "memory; `pageable`: numpy buffers through the engine's pinned staging copies"}
+                     "note": "SURVEY 8(d)'s step: items H2D, kernels, results D2H, rotated batches; the compiled "
+                             "submit/wait loop (libgck_driver.so gckd_run_host) over host buffers in pinned memory "
+                             "(gck_host_alloc: 20-B items DMA'd from them, 1+4 B results DMA'd into them); "
+                             "`python_pinned`: the same through one ctypes call per submit/wait; `pageable`: numpy "
+                             "buffers through the engine's pinned staging copies; `one_at_a_time`: 1 in flight"}
 
     progress("host-buffer runs done")
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------

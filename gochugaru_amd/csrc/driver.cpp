@@ -49,4 +49,34 @@ int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistenc
   return rc;
 }
 
+// The same loop over host buffers (no GCK_SUBMIT_DEVICE): items[k] / perm[k] / err[k] are host
+// pointers — gck_host_alloc memory moves by DMA straight from and into them — and each batch runs
+// on the engine's workspace stream: items H2D, kernels, results D2H.
+int gckd_run_host(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs, size_t n_batches,
+                  const uint64_t* items, const uint64_t* perm, const uint64_t* err, size_t n, uint32_t depth,
+                  int64_t now_us, double* seconds) {
+  if (depth == 0) depth = 1;
+  std::deque<gck_batch*> q;
+  int rc = GCK_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t k = 0; k < n_batches && rc == GCK_OK; ++k) {
+    if (q.size() >= depth) {
+      rc = wait(e, q.front());
+      q.pop_front();
+      if (rc != GCK_OK) break;
+    }
+    gck_batch* b = nullptr;
+    rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, now_us,
+                reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), 0u, nullptr, &b);
+    if (rc == GCK_OK) q.push_back(b);
+  }
+  while (!q.empty()) {
+    const int r = wait(e, q.front());
+    if (rc == GCK_OK) rc = r;
+    q.pop_front();
+  }
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
 }  // extern "C"

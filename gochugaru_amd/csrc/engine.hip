@@ -94,6 +94,10 @@ struct DeviceSnapshot {
   std::vector<unsigned char> cj_host;
   uint32_t cj_n_desc = 0, cj_o_meta = 0, cj_o_entries = 0;
   const unsigned char* d_cj = nullptr;
+  // label-join stage (labels.inc): root table + LjMeta[] (in the program block), slot words
+  std::vector<unsigned char> lj_host;
+  uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
+  const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
   uint8_t* cav_static = nullptr;  // per caveat instance (Engine::caveat_static)
@@ -1168,6 +1172,30 @@ static T* dalloc(std::vector<void*>& list, size_t count, uint64_t* bytes = nullp
   return static_cast<T*>(p);
 }
 
+// Runs f(lo, hi) over [0, n) on up to 16 host threads (one below `grain` items); the first
+// exception is rethrown.
+template <class F>
+static void host_parallel(size_t n, size_t grain, F&& f) {
+  const size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), (n + grain - 1) / grain});
+  if (nt <= 1) {
+    if (n) f(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  std::vector<std::exception_ptr> ex(nt);
+  for (size_t t = 0; t < nt; ++t)
+    ts.emplace_back([&, t] {
+      try {
+        f(n * t / nt, n * (t + 1) / nt);
+      } catch (...) {
+        ex[t] = std::current_exception();
+      }
+    });
+  for (auto& t : ts) t.join();
+  for (auto& x : ex)
+    if (x) std::rethrow_exception(x);
+}
+
 int device_init(Engine& e) {
   if (e.device_ready) return 0;
   int n = 0;
@@ -1321,6 +1349,7 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 #include "heights.inc"
 #include "closure.inc"
 #include "bidir.inc"
+#include "labels.inc"
 
 // Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
 // (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
@@ -1418,6 +1447,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     std::vector<DevNode> nodes = sc.nodes;
     build_heights(e, *ds, nodes, items, table, info, adopted, delta);
     build_bidir(e, *ds, nodes, items, table, info, adopted);
+    build_labels(e, *ds, nodes, items, table, info);
     for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
       if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
     ds->table = table;
@@ -1450,6 +1480,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     const size_t o_cst = put(cst.data(), cst.size());
     const size_t o_crow = put(crow.data(), crow.size() * 4);
     const size_t o_cj = ds->cj_host.empty() ? 0 : put(ds->cj_host.data(), ds->cj_host.size());
+    const size_t o_lj = ds->lj_host.empty() ? 0 : put(ds->lj_host.data(), ds->lj_host.size());
     std::vector<unsigned long long> hp(ds->hgt.size());  // heights array of each forward node
     for (size_t n = 0; n < hp.size(); ++n) hp[n] = (unsigned long long)(uintptr_t)ds->hgt[n];
     const size_t o_hgt = put(hp.data(), hp.size() * 8);
@@ -1463,6 +1494,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     ds->cav_row = reinterpret_cast<uint32_t*>(d_blob + o_crow);
     ds->d_hgt = reinterpret_cast<const unsigned long long*>(d_blob + o_hgt);
     ds->d_cj = ds->cj_host.empty() ? nullptr : d_blob + o_cj;
+    ds->d_lj = ds->lj_host.empty() ? nullptr : d_blob + o_lj;
     ds->node_bits = std::max<uint32_t>(1, ceil_log2(sc.nodes.size()));
     if (ds->node_bits > 12) throw Error(GCK_E_SCHEMA, "schema too large for the visited-key layout");
     ds->q_bits = 31 - ds->node_bits;
@@ -1971,8 +2003,43 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // counted in the published counters and bundled by bundles_finish, so the common batch is two
   // launches: the join and the publication
   const DeviceSnapshot& ds = *e.dev;
-  w.b_closure = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
-  if (w.b_closure) {
+  const bool cj = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
+  const bool lj = !cj && ds.d_lj;
+  w.b_closure = cj || lj;
+  if (lj) {
+    // the label join (labels.inc): one round of slot lines per check; what it leaves goes to the
+    // wave bundles through the same deferred list as the closure join's
+    LjArgs j{};
+    j.items = d_items;
+    j.n = n;
+    j.out_perm = d_perm;
+    j.out_err = d_err;
+    j.deferred = w.c_deferred;
+    j.n_deferred = w.b_ctrs + 4;
+    j.table = ds.d_lj;
+    j.n_fwd = ds.n_fwd;
+    j.table_bytes = (uint32_t)((ds.lj_host.size() + 3) & ~(size_t)3);
+    j.o_meta = ds.lj_o_meta;
+    if (!host_out && !w.b_own_stream) {  // self-published (see the closure join below)
+      j.pub = reinterpret_cast<unsigned*>(w.ctr);
+      j.pub_words = kPubWords;
+      j.h_out = w.d_hpub;
+      j.done = w.b_ctrs + kBDone;
+      j.seq = ++w.pub_seq;
+      w.b_seq = j.seq;
+    }
+    const dim3 grid((n + 32u * kWaves - 1) / (32u * kWaves)), block(kBlock);
+    hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
+    if (ds.lj_bits == 24 && ds.lj_sw == 16)
+      hipExtLaunchKernelGGL((k_label_join<24, 16>), grid, block, 0, st, e0, e1, 0, j);
+    else if (ds.lj_bits == 24)
+      hipExtLaunchKernelGGL((k_label_join<24, 32>), grid, block, 0, st, e0, e1, 0, j);
+    else if (ds.lj_sw == 16)
+      hipExtLaunchKernelGGL((k_label_join<32, 16>), grid, block, 0, st, e0, e1, 0, j);
+    else
+      hipExtLaunchKernelGGL((k_label_join<32, 32>), grid, block, 0, st, e0, e1, 0, j);
+    HIP_OK(hipGetLastError());
+  } else if (cj) {
     CjArgs j{};
     j.items = d_items;
     j.n = n;
@@ -2299,32 +2366,6 @@ static void stage_caveats(Workspace& w, CavCall&& call, hipStream_t st) {
   HIP_OK(hipMemsetAsync(w.req_set, 0xFF, (size_t)kReqSet * 8, st));
   HIP_OK(hipMemsetAsync(w.req_cnt, 0, 4, st));
   upload_cav_map(w, st);
-}
-
-// Evaluates the recorded pairs (row << 32 | slot) on the host, in parallel above a few hundred;
-// an evaluation error is outcome 3.
-// Runs f(lo, hi) over [0, n) on up to 16 host threads (one below `grain` items); the first
-// exception is rethrown.
-template <class F>
-static void host_parallel(size_t n, size_t grain, F&& f) {
-  const size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), (n + grain - 1) / grain});
-  if (nt <= 1) {
-    if (n) f(0, n);
-    return;
-  }
-  std::vector<std::thread> ts;
-  std::vector<std::exception_ptr> ex(nt);
-  for (size_t t = 0; t < nt; ++t)
-    ts.emplace_back([&, t] {
-      try {
-        f(n * t / nt, n * (t + 1) / nt);
-      } catch (...) {
-        ex[t] = std::current_exception();
-      }
-    });
-  for (auto& t : ts) t.join();
-  for (auto& x : ex)
-    if (x) std::rethrow_exception(x);
 }
 
 // Evaluates the recorded pairs (row << 32 | slot) on the host, parsing the contexts they need

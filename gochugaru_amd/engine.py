@@ -59,6 +59,7 @@ FLAG_NO_BIDIR = 16
 FLAG_NO_CLOSURE = 32
 FLAG_LAZY_CAVEATS = 64
 FLAG_NO_SLOTS = 128
+FLAG_NO_LABELS = 256
 SUBMIT_DEVICE = 1
 SUBMIT_ENGINE_STREAM = 2
 
@@ -216,6 +217,9 @@ def _driver():
         d.gckd_run.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int64,
                                C.POINTER(C.c_double)]
+        d.gckd_run_host.restype = C.c_int
+        d.gckd_run_host.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_size_t, C.c_uint32, C.c_int64, C.POINTER(C.c_double)]
         _DRIVER = d
     return _DRIVER
 
@@ -267,12 +271,13 @@ class Engine:
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
                  giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
                  bidir: bool = True, bidir_both: int = 0, workspaces: int = 0, closure: bool = True,
-                 lazy_caveats: bool = False, slots: bool = True):
+                 lazy_caveats: bool = False, slots: bool = True, labels: bool = True):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
                  | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
                  | (0 if bidir else FLAG_NO_BIDIR) | (0 if closure else FLAG_NO_CLOSURE)
-                 | (FLAG_LAZY_CAVEATS if lazy_caveats else 0) | (0 if slots else FLAG_NO_SLOTS))
+                 | (FLAG_LAZY_CAVEATS if lazy_caveats else 0) | (0 if slots else FLAG_NO_SLOTS)
+                 | (0 if labels else FLAG_NO_LABELS))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,
@@ -554,6 +559,13 @@ class Engine:
         """GCK_FLAG_PROFILE for the batches submitted from now on (gck_set_profile)."""
         _check(self._lib.gck_set_profile(self._h, 1 if on else 0))
 
+    def prepare_batches(self, items, perms, errs, n: int, depth: int, streams=None, engine_streams: bool = False,
+                        now_us: int = 0, host: bool = False) -> "PreparedRun":
+        """The arguments of one compiled submit/wait loop (libgck_driver.so), marshalled ahead, so
+        that a timed region holds the C loop alone. host=True: items / perms / errs are host
+        pointers (gck_host_alloc memory for DMA in place), batches on the engine's streams."""
+        return PreparedRun(self, items, perms, errs, n, depth, streams, engine_streams, now_us, host)
+
     def run_device_batches(self, items, perms, errs, n: int, depth: int, streams, engine_streams: bool = False,
                            now_us: int = 0) -> float:
         """Checks len(items) device batches of n items each (device pointers items[k], perms[k],
@@ -711,6 +723,34 @@ class Engine:
             if items[i]["subject_type"] == TYPE_INVALID:
                 items[i]["subject_id"] = ID_WILDCARD if r.SubjectID == "*" else ID_ABSENT
         return items
+
+
+class PreparedRun:
+    """A compiled submit/wait loop with its argument arrays built (Engine.prepare_batches)."""
+
+    def __init__(self, engine, items, perms, errs, n, depth, streams, engine_streams, now_us, host):
+        arr = lambda xs: (C.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
+        self._e, self._k, self._n, self._depth, self._now, self._host = engine, len(items), n, depth, now_us, host
+        self._items, self._perms, self._errs = arr(items), arr(perms), arr(errs)
+        self._streams = arr(streams or [0])
+        self._flags = SUBMIT_ENGINE_STREAM if engine_streams else 0
+        self._cs = _Consistency(CONSISTENCY_MIN_LATENCY, 0, 0)
+        self._drv = _driver()
+        self._submit = C.cast(engine._lib.gck_check_submit, C.c_void_p)
+        self._wait = C.cast(engine._lib.gck_check_wait, C.c_void_p)
+        self._secs = C.c_double(0.0)
+
+    def run(self) -> float:
+        """Runs the loop; returns its wall time in seconds (first submit to last wait)."""
+        if self._host:
+            _check(self._drv.gckd_run_host(self._submit, self._wait, self._e._h, C.byref(self._cs), self._k,
+                                           self._items, self._perms, self._errs, self._n, self._depth, self._now,
+                                           C.byref(self._secs)))
+        else:
+            _check(self._drv.gckd_run(self._submit, self._wait, self._e._h, C.byref(self._cs), self._k, self._items,
+                                      self._perms, self._errs, self._n, self._depth, self._streams, self._flags,
+                                      self._now, C.byref(self._secs)))
+        return self._secs.value
 
 
 class Batch:

@@ -113,6 +113,8 @@ extern "C" {
                                     the bundle search) */
 #define GCK_FLAG_NO_SLOTS 128u  /* gck_config.flags: no per-user / per-resource slots for the
                                    closure join (saves ~128 B per user of HBM; slower) */
+#define GCK_FLAG_NO_LABELS 256u  /* gck_config.flags: no label-join stage (hub hierarchy labels and
+                                    flattened resource slots; labels.inc) */
 #define GCK_FLAG_LAZY_CAVEATS 64u /* gck_config.flags: always evaluate check-time caveat contexts
                                      lazily (only the pairs a walk meets; by default a call whose
                                      partial instances x distinct contexts is small evaluates them all) */

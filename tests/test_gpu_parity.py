@@ -171,32 +171,38 @@ PATHS = {
     # grid-wide level-synchronous kernels only
     "wide": {"wide_only": True},
     # the bundle machinery on its own (no closure-join stage) ...
-    "noclosure": {"closure": False},
+    "noclosure": {"closure": False, "labels": False},
     # tiny per-wave scratch: most bundles overflow and are re-run by the later stages
-    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 8, "closure": False},
+    "bundle-deferred": {"bundle_checks": 3, "bundle_frontier": 8, "bundle_visited": 8, "closure": False, "labels": False},
     # tiny work budget: almost every check is handed to a 16-wave workgroup bundle
-    "giant": {"bundle_budget": 2, "closure": False},
+    "giant": {"bundle_budget": 2, "closure": False, "labels": False},
     # ... and those overflow their workgroup scratch into the grid-wide path
     "giant-deferred": {"bundle_budget": 2, "giant_frontier": 8, "giant_visited": 16, "giant_slots": 3,
-                       "closure": False},
+                       "closure": False, "labels": False},
     # deferred checks straight to the grid-wide path
-    "giant-skip": {"bundle_budget": 2, "giant_stage": False, "closure": False},
+    "giant-skip": {"bundle_budget": 2, "giant_stage": False, "closure": False, "labels": False},
     # what the closure-join stage leaves goes through the bundles' deferral chain
     "closure-giant": {"bundle_budget": 2},
     # the closure join's task rounds alone (no user / resource slots)
     "noslots": {"slots": False},
     # one check per wavefront, few resident waves
-    "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4, "closure": False},
+    "bundle-1": {"bundle_checks": 1, "bundle_waves_per_cu": 4, "closure": False, "labels": False},
     # binary-search membership instead of the hashed index, both paths
-    "nohash": {"membership_hash": False},
+    "nohash": {"membership_hash": False, "labels": False},
     "nohash-wide": {"membership_hash": False, "wide_only": True},
     # forward-only wave bundles (no bidirectional checks, hence no closure join)
-    "nobidir": {"bidir": False},
+    "nobidir": {"bidir": False, "labels": False},
     # bidirectional checks always expanding only the smaller side (most carrying) ...
-    "bidir-one": {"bidir_both": 1, "closure": False},
+    "bidir-one": {"bidir_both": 1, "closure": False, "labels": False},
     # ... or always both sides; and bidirectional checks deferred to the later stages
-    "bidir-all": {"bidir_both": 1 << 30, "closure": False},
-    "bidir-deferred": {"bundle_budget": 6, "bundle_frontier": 16, "bundle_visited": 64, "closure": False},
+    "bidir-all": {"bidir_both": 1 << 30, "closure": False, "labels": False},
+    "bidir-deferred": {"bundle_budget": 6, "bundle_frontier": 16, "bundle_visited": 64, "closure": False, "labels": False},
+    # the label join (labels.inc) for every root it takes, the nested-group ones included ...
+    "labels": {"closure": False},
+    # ... with its leftovers through the bundles' deferral chain
+    "labels-deferred": {"closure": False, "bundle_budget": 2},
+    # no label join: the default stage A of round 2 (closure join, then bundles)
+    "nolabels": {"labels": False},
 }
 
 
@@ -224,6 +230,8 @@ def test_random_parity(family, seed, path):
         assert e.stats()["slot_checks"] > 0  # doc#view@user decided from the slots
     if path == "noslots":
         assert e.stats()["slot_checks"] == 0
+    if path == "labels" and family in ("nested", "gdocs", "github", "gdocs_deep"):
+        assert e.stats()["slot_checks"] > 0  # decided by the label join's slots
     if path == "noclosure" and family in ("nested", "gdocs_deep"):
         assert e.stats()["bidir_checks"] > 0 and e.stats()["closure_checks"] == 0
     if path in ("nobidir", "wide") or family == "caveated":
