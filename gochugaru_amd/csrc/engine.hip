@@ -1216,6 +1216,24 @@ int device_init(Engine& e) {
   return 0;
 }
 
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+PhaseClock::PhaseClock(const char* w) : what(w), on(getenv("GCK_DEBUG_PHASES") != nullptr), t0(0), last(0) {
+  if (on) t0 = last = now_s();
+}
+void PhaseClock::mark(const char* phase) {
+  if (!on) return;
+  const double t = now_s();
+  char buf[96];
+  snprintf(buf, sizeof(buf), " %s=%.1fus", phase, (t - last) * 1e6);
+  line += buf;
+  last = t;
+}
+PhaseClock::~PhaseClock() {
+  if (on) fprintf(stderr, "[gck %s] total=%.1fus%s\n", what, (now_s() - t0) * 1e6, line.c_str());
+}
+
 static void free_list(std::vector<void*>& list) {
   for (void* p : list) (void)hipFreeAsync(p, nullptr);
   list.clear();
@@ -1356,6 +1374,7 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 // derived structures of unchanged CSRs. Taken-over arrays join the new snapshot's allocation
 // list only on success, so a failure frees nothing the previous snapshot still owns.
 void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
+  PhaseClock pc(delta ? "relink" : "upload");
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
   Schema& sc = *e.schema;
@@ -1445,9 +1464,13 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
       }
     }
     std::vector<DevNode> nodes = sc.nodes;
+    pc.mark("csrs");
     build_heights(e, *ds, nodes, items, table, info, adopted, delta);
+    pc.mark("heights");
     build_bidir(e, *ds, nodes, items, table, info, adopted);
+    pc.mark("bidir");
     build_labels(e, *ds, nodes, items, table, info);
+    pc.mark("labels");
     for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
       if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
     ds->table = table;
@@ -1501,6 +1524,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     // exact-depth layout (make_ctx): tag 2 bits, depth, node, query id below bit 63
     const uint32_t md = e.cfg.max_depth ? e.cfg.max_depth : 50;
     ds->q_bits_deep = 63 - (34 + ceil_log2((uint64_t)md + 1) + ds->node_bits);
+    pc.mark("program");
   } catch (...) {
     free_list(ds->allocs);
     for (void* p : ds->hallocs) (void)hipFree(p);

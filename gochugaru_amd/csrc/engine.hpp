@@ -200,6 +200,17 @@ struct Engine {
   ~Engine();
 };
 
+// GCK_DEBUG_PHASES=1: wall time of the snapshot / Watch phases on stderr (engine.hip PhaseClock)
+struct PhaseClock {
+  const char* what;
+  bool on;
+  double t0, last;
+  std::string line;
+  explicit PhaseClock(const char* w);
+  void mark(const char* phase);
+  ~PhaseClock();
+};
+
 // snapshot.cpp
 void add_tuples_text(Engine& e, const char* text, size_t len);
 // gck_api.cpp: caveat instances (a caveat name + stored context)

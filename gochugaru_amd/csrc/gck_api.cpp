@@ -498,10 +498,13 @@ static void apply_updates(Engine& e, uint64_t revision, const std::vector<gck_up
       if (part_owner(u.tuple.resource_id, e.part_world) == e.part_rank) mine.push_back(u);
     use = &mine;
   }
+  PhaseClock pc("watch");
   std::vector<UpdateGroup> groups = group_updates(e, *use);
+  pc.mark("group");
   if (!groups.empty()) {
     try {
       device_apply(e, groups);
+      pc.mark("device");
     } catch (...) {
       e.committed = false;
       throw;
