@@ -123,7 +123,9 @@ def test_resources_at_the_budget_are_deferred():
         _run(schema, tuples, checks, max_depth=gen.FAMILY_DEPTH.get("near_budget", 50))
 
 
-def test_cyclic_hierarchy_disables_labels():
+def test_cyclic_hierarchy_condensed():
+    """Cycles in the group hierarchy are condensed (labels.inc hier_scc); resources that reach a
+    cycle sit at the depth budget and are deferred to the exact-depth path."""
     for seed in (1, 2):
         schema, tuples, checks = gen.cyclic(seed)
         _run(schema, tuples, checks, max_depth=gen.FAMILY_DEPTH.get("cyclic", 50))

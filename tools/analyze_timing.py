@@ -1,5 +1,5 @@
 """Debug helper: summarise GCK_DEBUG_TIMING=<prefix> records (per-bundle wall-clock spans).
-Usage: GCK_DEBUG_TIMING=/tmp/t python bench.py ... ; python tests/analyze_timing.py /tmp/t.bin"""
+Usage: GCK_DEBUG_TIMING=/tmp/t python bench.py ... ; python tools/analyze_timing.py /tmp/t.bin"""
 import sys
 
 import numpy as np

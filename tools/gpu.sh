@@ -1,0 +1,70 @@
+# GPU-box jobs in one parameterised tool (run under gpurun from the repo root; libraries are built
+# beforehand in the container). Every GPU step has its own time limit; a failing step ends the job.
+#
+#   bash tools/gpu.sh tests <tag> [pytest args]          pytest -m gpu (or the given files)
+#   bash tools/gpu.sh bench <tag> [bench args]           one bench.py line -> gpurun_out/<tag>/bench.json
+#   bash tools/gpu.sh sweep <tag> "<flags>" ...          one bench line per flag set (no oracle / CPU)
+#   bash tools/gpu.sh profile <tag> [bench args]         rocprofv3 kernel trace + stats (8 in flight and
+#                                                        1 in flight), then FETCH_SIZE and WRITE_SIZE
+#                                                        passes (separate runs), the gather-probe
+#                                                        calibration, and traffic.json
+#   bash tools/gpu.sh phases <tag> [bench args]          bench with GCK_DEBUG_PHASES=1 (snapshot / Watch
+#                                                        phase times on stderr)
+set -e
+CMD=$1
+TAG=$2
+shift 2 || true
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+case "$CMD" in
+  tests)
+    ARGS=${*:-tests -m gpu}
+    timeout -k 10 900 python -u -m pytest $ARGS -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 \
+      || { tail -40 "$OUT/pytest.log"; exit 1; }
+    tail -3 "$OUT/pytest.log"
+    ;;
+  bench)
+    timeout -k 10 600 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+    tail -c 600 "$OUT/bench.json"
+    ;;
+  phases)
+    GCK_DEBUG_PHASES=1 timeout -k 10 600 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
+      || { tail -20 "$OUT/bench.err"; exit 1; }
+    grep "\[gck" "$OUT/bench.err" | tail -20
+    ;;
+  sweep)
+    i=0
+    for cfg in "$@"; do
+      i=$((i+1))
+      timeout -k 10 300 python3 bench.py --no-oracle --no-cpu $cfg > "$OUT/s$i.json" 2> "$OUT/s$i.err"
+      echo "$cfg :: $(python3 -c "import json; d=json.load(open('$OUT/s$i.json')); print(d['value'], d.get('host_buffers', {}).get('value'))")"
+    done
+    ;;
+  profile)
+    GP=tools/gather_probe/gather_probe
+    if [ -x $GP ]; then
+      timeout -k 10 120 $GP > "$OUT/gather_plain.jsonl"
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/gfetch" -o gfetch --output-format csv -- $GP > "$OUT/gather_fetch.jsonl" 2> "$OUT/gather_fetch.err"
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/gwrite" -o gwrite --output-format csv -- $GP > "$OUT/gather_write.jsonl" 2> "$OUT/gather_write.err"
+      echo "calibration done"
+    fi
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --host-steps 0 "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt1" -o kt1 --output-format csv -- python3 bench.py --no-cpu --host-steps 0 --inflight 1 "$@" > "$OUT/kt1.json" 2> "$OUT/kt1.err"
+    echo "kernel trace done"
+    SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --no-cpu --host-steps 0 --inflight 1 $*"
+    timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- $SHORT > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+    timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- $SHORT > "$OUT/write.json" 2> "$OUT/write.err"
+    echo "pmc done"
+    python3 tools/traffic_summary.py "$OUT" > "$OUT/traffic.json" || true
+    cat "$OUT/traffic.json" || true
+    # keep the summaries; drop per-dispatch traces (gpurun_out copies back at most 64 MiB)
+    find "$OUT" -name "*kernel_trace.csv" -delete
+    find "$OUT" -name "*counter_collection.csv" -delete
+    find "$OUT" -name "*agent_info.csv" -delete
+    ;;
+  *)
+    echo "usage: tools/gpu.sh tests|bench|sweep|profile|phases <tag> [args]" >&2
+    exit 2
+    ;;
+esac

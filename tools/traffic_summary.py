@@ -1,4 +1,4 @@
-"""Per-batch HBM bytes of the check kernels, from tools/pmc_r02.sh output.
+"""Per-batch HBM bytes of the check kernels, from `tools/gpu.sh profile` output.
 
 FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived counters). MI355X_MICROARCH.md
 §HBM establishes FETCH_SIZE = 1/2 of the bytes for wide streaming reads only; tools/gather_probe
@@ -16,6 +16,8 @@ from collections import defaultdict
 def kernel_key(name):
     if "k_closure_join" in name:
         return "k_closure_join"
+    if "k_label_join" in name:
+        return "k_label_join"
     if "k_bundles<1," in name:
         return "k_bundles<1>"
     if "k_bundles<16," in name:
@@ -63,7 +65,7 @@ def main(out):
                         "write_reported": gw.get(k), "write_bytes": lanes * 4}
     fetch, n_fetch = per_kernel(f"{out}/fetch/**/*counter_collection.csv", "FETCH_SIZE")
     write, n_write = per_kernel(f"{out}/write/**/*counter_collection.csv", "WRITE_SIZE")
-    stage_a = [k for k in ("k_closure_join", "k_bundles<1>") if k in fetch]
+    stage_a = [k for k in ("k_closure_join", "k_label_join", "k_bundles<1>") if k in fetch]
     factor = (calib.get(64) or {}).get("factor") or 1.0  # one 64-B line per random access
     raw = sum(fetch[k] for k in stage_a)
     res = {
