@@ -91,12 +91,13 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     args = ap.parse_args()
     nested = args.config == "nested"
+    pipelined = args.config in ("nested", "gdocs", "github")  # batches in flight through the compiled loop
     if args.steps is None:
-        args.steps = 2000 if nested else 200
+        args.steps = 2000 if nested else (1000 if pipelined else 200)
     if args.warmup is None:
         args.warmup = 100 if nested else 20
     if args.inflight is None:
-        args.inflight = 8 if nested else 3
+        args.inflight = 8 if pipelined else 3
     # untimed batches before the timed region: at least --warmup, and at least two per batch in
     # flight, so that every workspace, stream and hardware queue has run a batch before t0
     args.warm = max(args.warmup, 2 * max(1, args.inflight))
