@@ -604,8 +604,18 @@ def main():
     if rank == 0 and not args.no_oracle and WL.kind == "mixed":
         from oracle import corc  # the final snapshot (after every Watch batch) vs the timed batch
         hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
-        cp, ce = WL.M.expected(hi, threads=threads)
+        mx = {}
+        cp, ce = WL.M.expected(hi, threads=threads, stats=mx)
         agree_mixed = float(((cp == res) & (ce == errs)).mean())
+        if not args.no_cpu and world == 1:
+            # the C oracle answering the timed batch once (each context class against the snapshot
+            # with its caveat outcomes), on the final snapshot; the Watch batches are not included
+            cpu_q = {"value": round(args.batch / mx["seconds"], 1), "unit": "checks/s", "cores": threads, "kind": "port",
+                     "sample": f"the timed batch ({args.batch} checks, 3 context classes), C oracle "
+                               f"(oracle/check_oracle.c; caveat outcomes per context class), OpenMP {cpu_note}, "
+                               f"{mx['seconds']:.2f}s; Watch application not included"}
+        # SURVEY §8d algorithmic bytes of one check batch (+4 B per caveated edge)
+        mixed_alg = 25 * args.batch + 8 * mx["rows"] + 4 * mx["edges"] + 4 * mx["cav_edges"]
     if rank == 0 and not args.no_oracle and WL.kind == "quota":
         from oracle import corc  # the first timed batch vs the C oracle's threshold mode
         q_threads = threads
@@ -741,8 +751,20 @@ def main():
     progress("oracle / CPU baseline done")
     if rank == 0 and WL.kind in ("mixed", "quota") and not args.no_oracle:
         agree = agree_mixed
-    if rank == 0 and WL.kind == "quota" and not args.no_oracle and not args.no_cpu and world == 1:
+    if rank == 0 and WL.kind in ("quota", "mixed") and not args.no_oracle and not args.no_cpu and world == 1:
         cpu = cpu_q
+    if rank == 0 and WL.kind == "mixed" and not args.no_oracle and st["bundle_launches"] and st["bundle_ms"] > 0:
+        # config 5: the check batch's stage A (wave bundles with caveat outcomes) timed by its HIP
+        # events every 4th batch of a workspace inside the timed region; the Watch batch is
+        # the rest of the step (watch.apply_ms_per_step)
+        ms_a = (st["bundle_ms"] + st["giant_ms"]) / st["bundle_launches"]
+        achieved = mixed_alg / (ms_a * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "kernel": "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks), "
+                          "HIP events on its launch stream, sampled every 4th batch in the timed region",
+                "alg_bytes_per_launch": int(mixed_alg), "mean_launch_ms": round(ms_a, 4),
+                "achieved_job": round(mixed_alg * args.steps / elapsed / 1e9, 3)}
 
     if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
         cp, ce, _ = corc.check(prog, tab, host_items, threads=threads)

@@ -97,6 +97,7 @@ struct DeviceSnapshot {
   // label-join stage (labels.inc): root table + LjMeta[] (in the program block), slot words
   std::vector<unsigned char> lj_host;
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
+  bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
   const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
@@ -133,6 +134,7 @@ struct Workspace {
   int32_t* b_xerr = nullptr;  // the caller's buffers themselves when they are gck_host_alloc memory
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
   bool b_closure = false;     // stage A began with the closure join: its leftovers are bundled in finish
+  bool b_chained = false;     // ... or already in stage A, by bundles chained on the device
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
@@ -2027,9 +2029,16 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // counted in the published counters and bundled by bundles_finish, so the common batch is two
   // launches: the join and the publication
   const DeviceSnapshot& ds = *e.dev;
-  const bool cj = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
-  const bool lj = !cj && ds.d_lj;
+  const bool cj_ok = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
+  const bool lj = ds.d_lj && (!cj_ok || ds.lj_preferred);
+  const bool cj = cj_ok && !lj;
   w.b_closure = cj || lj;
+  // chained: the wave bundles over the join's deferred list follow it in stage A, reading the
+  // list's length on the device — no host round trip in the wait — when recent batches of the
+  // engine left checks (a persistent bundle launch over an empty list costs a few microseconds,
+  // the round trip tens; engine.hpp Engine::defer_recent)
+  w.b_chained = w.b_closure && e.defer_recent.load(std::memory_order_relaxed) > 0;
+  const bool self_pub = !host_out && !w.b_own_stream && !w.b_chained;
   if (lj) {
     // the label join (labels.inc): one round of slot lines per check; what it leaves goes to the
     // wave bundles through the same deferred list as the closure join's
@@ -2044,7 +2053,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.n_fwd = ds.n_fwd;
     j.table_bytes = (uint32_t)((ds.lj_host.size() + 3) & ~(size_t)3);
     j.o_meta = ds.lj_o_meta;
-    if (!host_out && !w.b_own_stream) {  // self-published (see the closure join below)
+    if (self_pub) {  // self-published (see the closure join below)
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
       j.h_out = w.d_hpub;
@@ -2084,7 +2093,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     // its reads — the join's end (k_publish after it sees every block's results written back
     // past the L2s; the join's own last block sees only that every block has decided: a host-side
     // stream query or synchronisation per batch instead costs ~10 us, 11 G -> 3-5 G checks/s)
-    if (!host_out && !w.b_own_stream) {
+    if (self_pub) {
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
       j.h_out = w.d_hpub;
@@ -2118,11 +2127,17 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     launch_wave_bundles(e, w, c, a, st);
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
   }
+  if (w.b_chained) {
+    BundleArgs b = a;
+    b.idx = w.c_deferred;
+    b.n_dev = w.b_ctrs + 4;
+    launch_wave_bundles(e, w, c, b, st);
+  }
   if (host_out) {
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
-  if (!w.b_closure || host_out || w.b_own_stream) publish_launch(w, st);
+  if (!self_pub || !w.b_closure) publish_launch(w, st);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
@@ -2150,7 +2165,12 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     e.stats.closure_checks += n - n_cj;
     e.stats.slot_checks += n - n_cj - tasks;
   }
-  if (n_cj > 0) {
+  // recent batches with leftovers make the next ones chain their bundles on the device
+  if (w.b_closure) {
+    if (n_cj > 0) e.defer_recent.store(16, std::memory_order_relaxed);
+    else if (e.defer_recent.load(std::memory_order_relaxed) > 0) e.defer_recent.fetch_sub(1, std::memory_order_relaxed);
+  }
+  if (n_cj > 0 && !w.b_chained) {
     // the checks the closure join left: the wave bundles over its list (the publish zeroed the
     // count on the device: restore it first)
     Ctx c = make_ctx(e, w, now_us);

@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <shared_mutex>
@@ -197,6 +198,9 @@ struct Engine {
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
   size_t delta_scratch_cap = 0;
   gck_stats stats{};
+  // batches to come that chain the wave bundles behind the join in stage A (engine.hip
+  // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none
+  std::atomic<int> defer_recent{0};
   ~Engine();
 };
 

@@ -222,3 +222,124 @@ def host_arrays(G: Graph) -> Dict[str, np.ndarray]:
             t = t.to(torch.int32)
         out[name] = t.cpu().numpy().view(np.uint32)
     return out
+
+
+class NestedChurn:
+    """Watch churn on the config-4 graph (client/client.go:370-413 UpdatesSinceRevision: CREATE /
+    TOUCH / DELETE of relationships) with the graph's state kept on the host as sorted
+    (object << 32 | subject) keys per relation kind, so that the C oracle can check any revision.
+    Updates hit all three kinds: user memberships, group nesting (acyclic: a parent in a higher
+    layer) and document viewers; `cycle=True` adds one nesting edge from a deep descendant back up
+    to a group above it, which closes a cycle in the hierarchy."""
+
+    KINDS = [(R_MEMBER, T_USER, ELLIPSIS), (R_MEMBER, T_GROUP, R_MEMBER), (R_VIEWER, T_GROUP, R_MEMBER)]
+
+    def __init__(self, G: Graph, seed: int = 99):
+        self.G = G
+        self.rng = np.random.default_rng(seed)
+        H = host_arrays(G)
+        self.rows = {R_MEMBER: G.n_groups, R_VIEWER: G.n_docs}
+        self.layer_start = G.layer_start.cpu().numpy()
+        self.keys = {}
+        for kind, (o, nb) in zip(self.KINDS, (("mem_user_off", "mem_user_nbr"), ("mem_group_off", "mem_group_nbr"),
+                                              ("viewer_off", "viewer_nbr"))):
+            off, nbr = H[o].astype(np.int64), H[nb].astype(np.uint64)
+            row = np.repeat(np.arange(off.size - 1, dtype=np.uint64), np.diff(off))
+            self.keys[kind] = (row << np.uint64(32)) | nbr  # rows ascending, sorted within: sorted
+
+    def _layer_of(self, g):
+        return np.searchsorted(self.layer_start, g, side="right") - 1
+
+    def batch(self, n: int, cycle: bool = False):
+        from gochugaru_amd.engine import UPDATE_CREATE, UPDATE_DELETE, UPDATE_DTYPE, UPDATE_TOUCH
+        rng, G = self.rng, self.G
+        share = [0.9, 0.05, 0.05]
+        out = []
+        for kind, frac in zip(self.KINDS, share):
+            rel, st, sr = kind
+            k = max(1, int(n * frac))
+            keys = self.keys[kind]
+            ops = rng.choice([UPDATE_CREATE, UPDATE_TOUCH, UPDATE_DELETE], size=k, p=[0.45, 0.45, 0.10])
+            n_new = int((ops == UPDATE_CREATE).sum())
+            rows = rng.integers(0, self.rows[rel], n_new)
+            if kind == (R_MEMBER, T_USER, ELLIPSIS):
+                subj = rng.integers(0, G.n_users, n_new)
+            elif kind == (R_MEMBER, T_GROUP, R_MEMBER):
+                # a parent in a higher layer than the child: the hierarchy stays acyclic
+                lay = self._layer_of(rows)
+                deeper = lay + 1 < self.layer_start.size - 1
+                lo = self.layer_start[np.minimum(lay + 1, self.layer_start.size - 2)]
+                subj = lo + (rng.random(n_new) * (G.n_groups - lo)).astype(np.int64)
+                subj = np.where(deeper, subj, -1)
+            else:
+                subj = rng.integers(0, G.n_groups, n_new)
+            new = (rows.astype(np.uint64) << np.uint64(32)) | subj.astype(np.uint64)
+            new = new[subj >= 0]
+            old = keys[rng.integers(0, keys.size, k - n_new)] if keys.size else np.zeros(0, np.uint64)
+            ukeys = np.concatenate([new, old])
+            uops = np.concatenate([ops[ops == UPDATE_CREATE][: new.size], ops[ops != UPDATE_CREATE]])
+            if cycle and kind == (R_MEMBER, T_GROUP, R_MEMBER):
+                ukeys, uops = self._with_cycle(ukeys, uops)
+            ukeys, first = np.unique(ukeys, return_index=True)
+            uops = uops[first]
+            # host state: drop every updated key, insert the upserts (both sides sorted: O(n) copies)
+            pos = np.searchsorted(keys, ukeys)
+            hit = (pos < keys.size) & (keys[np.minimum(pos, max(keys.size - 1, 0))] == ukeys)
+            keep = np.ones(keys.size, dtype=bool)
+            keep[pos[hit]] = False
+            kept = keys[keep]
+            up = uops != UPDATE_DELETE
+            ins = ukeys[up]
+            self.keys[kind] = np.insert(kept, np.searchsorted(kept, ins), ins)
+            u = np.zeros(ukeys.size, dtype=UPDATE_DTYPE)
+            u["op"] = uops
+            t = u["tuple"]
+            t["resource_type"] = T_GROUP if rel == R_MEMBER else T_DOC
+            t["relation"] = rel
+            t["resource_id"] = ukeys >> np.uint64(32)
+            t["subject_type"] = st
+            t["subject_relation"] = sr
+            t["subject_id"] = ukeys & np.uint64(0xFFFFFFFF)
+            u["tuple"] = t
+            out.append(u)
+        return np.concatenate(out)
+
+    def _with_cycle(self, ukeys, uops):
+        """One CREATE of `D#member@A#member` where D descends from A: A -> ... -> D -> A."""
+        from gochugaru_amd.engine import UPDATE_CREATE
+        keys = self.keys[(R_MEMBER, T_GROUP, R_MEMBER)]
+        rows = (keys >> np.uint64(32)).astype(np.int64)
+        a = int(rows[self.rng.integers(0, rows.size)])
+        d = a
+        for _ in range(6):  # walk down first children
+            lo = np.searchsorted(rows, d)
+            if lo >= rows.size or rows[lo] != d:
+                break
+            d = int(keys[lo] & np.uint64(0xFFFFFFFF))
+        if d == a:
+            return ukeys, uops
+        self.cycle = (a, d)
+        k = np.uint64((d << 32) | a)
+        return np.concatenate([ukeys, [k]]), np.concatenate([uops, [UPDATE_CREATE]])
+
+    def csrs(self):
+        """Host CSRs of the current state, in Graph.csrs() order (uint32 offsets / neighbours)."""
+        out = []
+        for kind in self.KINDS:
+            rel = kind[0]
+            keys = self.keys[kind]
+            n_rows = self.rows[rel]
+            off = np.zeros(n_rows + 1, dtype=np.uint32)
+            off[1:] = np.cumsum(np.bincount((keys >> np.uint64(32)).astype(np.int64), minlength=n_rows))
+            out.append((off, (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), n_rows))
+        return out
+
+    def oracle(self):
+        """(program, CSR table) of the C oracle over the current state."""
+        from oracle import corc
+        from oracle import spicedb_ref as ref
+        ids = corc.Ids(ref.Schema(SCHEMA))
+        idx = {(R_MEMBER, T_USER, ELLIPSIS, False): 0, (R_MEMBER, T_GROUP, R_MEMBER, False): 1,
+               (R_VIEWER, T_GROUP, R_MEMBER, False): 2}
+        tab = corc.make_csr_table([(off, nbr, None, None, n) for off, nbr, n in self.csrs()])
+        return corc.encode_program(ids, idx), tab

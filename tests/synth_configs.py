@@ -377,10 +377,16 @@ class Mixed:
         return np.concatenate(out)
 
     # ---- expected answers ------------------------------------------------------------------------
-    def expected(self, items_host: np.ndarray, threads: int = 16):
-        """(perm, err) for items whose context_slot is 0 (none), 1 (tuesday) or 2 (monday)."""
+    def expected(self, items_host: np.ndarray, threads: int = 16, stats: dict = None):
+        """(perm, err) for items whose context_slot is 0 (none), 1 (tuesday) or 2 (monday).
+        `stats` (a dict) receives the oracle's work on the items of each context class only —
+        `seconds` (the C oracle's time answering the batch once), `rows` / `edges` /
+        `cav_edges` (its counting, for SURVEY §8d's algorithmic bytes)."""
         res = []
-        for mode in ("cond", "true", "false"):
+        slot = items_host["context_slot"]
+        if stats is not None:
+            stats.update(seconds=0.0, rows=0, edges=0, cav_edges=0)
+        for m, mode in enumerate(("cond", "true", "false")):
             idx, arrays = {}, []
             for rid, st, sr, n_rows, off, nbr in self.static:
                 idx[(rid, st, sr, False)] = len(arrays)
@@ -397,8 +403,18 @@ class Mixed:
                     idx[(rid, st, sr, True)] = len(arrays)
                     arrays.append((off, nbr, np.ones(nbr.size, np.uint32), np.zeros(nbr.size, np.int64), n_rows))
             prog = corc.encode_program(self.W.ids, idx)
-            res.append(corc.check(prog, corc.make_csr_table(arrays), items_host, threads=threads)[:2])
-        slot = items_host["context_slot"]
+            tab = corc.make_csr_table(arrays)
+            res.append(corc.check(prog, tab, items_host, threads=threads)[:2])
+            if stats is not None:
+                import time
+                sub = items_host[slot == m]
+                if sub.size:
+                    t0 = time.perf_counter()
+                    _, _, cnt = corc.check(prog, tab, sub, threads=threads)
+                    stats["seconds"] += time.perf_counter() - t0
+                    stats["rows"] += cnt["rows"]
+                    stats["edges"] += cnt["edges"]
+                    stats["cav_edges"] += cnt.get("ext_edges", 0)
         perm = np.where(slot == 1, res[1][0], np.where(slot == 2, res[2][0], res[0][0]))
         err = np.where(slot == 1, res[1][1], np.where(slot == 2, res[2][1], res[0][1]))
         return perm, err
