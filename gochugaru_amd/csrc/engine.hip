@@ -98,6 +98,7 @@ struct DeviceSnapshot {
   std::vector<unsigned char> lj_host;
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
+  bool part_full = false;     // partitioned engine, first snapshot: every row present until part_finish_upload
   const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
@@ -1243,6 +1244,9 @@ static void free_list(std::vector<void*>& list) {
 
 static void free_part(PartState* p);  // partition.inc
 static void partition_filter(const Engine& e, DeviceSnapshot& ds, DevCSR& d, uint64_t& ne);
+struct CsrInfo;
+static void part_finish_upload(Engine& e, DeviceSnapshot& ds, std::vector<DevNode>& nodes, std::vector<DevCSR>& table,
+                               std::vector<CsrInfo>& info, const std::vector<size_t>& later);
 
 static void free_workspace(Workspace* w) {
   if (w->stream) (void)hipStreamSynchronize(w->stream);
@@ -1385,6 +1389,11 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
   try {
     std::vector<DevCSR> table;
     std::vector<CsrInfo> info;
+    // a partitioned engine's first snapshot: the heights and the label tables (labels.inc: the
+    // replicated hierarchy labels, the slots of this rank's subjects and resources) are built from
+    // every row as loaded, then each CSR keeps the rows this rank owns
+    std::vector<size_t> part_later;
+    ds->part_full = e.part_world > 1 && !delta;
     for (HostCSR& h : csrs) {
       DevCSR d{};
       d.n_rows = h.n_rows;
@@ -1437,9 +1446,15 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
         d.cav = cav;
         d.exp_us = ex;
       }
-      if (e.part_world > 1) {  // partitioned graph: keep the rows this rank owns (partition.inc)
+      if (e.part_world > 1 && delta) {  // partitioned graph: keep the rows this rank owns (partition.inc)
         partition_filter(e, *ds, d, ne);
         b.n_edges = ne;
+      } else if (e.part_world > 1) {  // ... after the label tables are built from every row (below)
+        part_later.push_back(table.size());
+        table.push_back(d);
+        info.push_back({ne, h.stype});
+        ds->base.push_back(b);
+        continue;
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
@@ -1473,6 +1488,7 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     pc.mark("bidir");
     build_labels(e, *ds, nodes, items, table, info);
     pc.mark("labels");
+    if (ds->part_full) part_finish_upload(e, *ds, nodes, table, info, part_later);
     for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
       if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
     ds->table = table;
@@ -2746,6 +2762,7 @@ static PartState& part_state(Workspace& w) {
 static void free_part(PartState* p) {
   if (!p) return;
   free_xfer(p->xfer);
+  free_join(p->pj);
   if (p->h_out) (void)hipHostFree(p->h_out);
   delete p;  // outbox / out_cnt are in the workspace's allocation list
 }

@@ -292,6 +292,12 @@ void part_init(Engine& e, const uint8_t* id);
 void part_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm, int32_t* d_err,
                 void* stream);
 void part_comm_free(Engine& e);
+// the partitioned label join (partition.inc): records (check, user slot) for the owners of the
+// resources, and their decision there
+void part_join_pack(Engine& e, const gck_item* d_items, size_t n, void* d_send, size_t send_cap, uint64_t* counts,
+                    void* stream);
+void part_join_decide(Engine& e, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv, uint8_t* d_perm,
+                      int32_t* d_err, void* stream);
 void device_free(Engine& e);
 
 }  // namespace gck

@@ -851,6 +851,29 @@ int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
   });
 }
 
+int gck_part_join_pack(gck_engine* ge, const gck_item* d_items, size_t n, void* d_send, size_t send_cap,
+                       uint64_t* send_counts, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(send_counts && (n == 0 || d_items) && (d_send || !send_cap), GCK_E_INVALID_ARGUMENT, "null argument");
+    part_join_pack(e, d_items, n, d_send, send_cap, send_counts, stream);
+  });
+}
+
+int gck_part_join_decide(gck_engine* ge, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv,
+                         uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE((n == 0 || (d_items && d_out_perm && d_out_err)) && (d_recv || !n_recv), GCK_E_INVALID_ARGUMENT,
+            "null argument");
+    part_join_decide(e, d_items, n, d_recv, n_recv, d_out_perm, d_out_err, stream);
+  });
+}
+
 int gck_part_unique_id(uint8_t* out) {
   return guard([&] {
     REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null id buffer");

@@ -193,6 +193,8 @@ _SIGS = {
     "gck_part_ingest": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "gck_part_resolve": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "gck_part_finish": (C.c_int, [_P, _P, _P]),
+    "gck_part_join_pack": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t, C.POINTER(C.c_uint64), _P]),
+    "gck_part_join_decide": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t, _P, _P, _P]),
     "gck_part_unique_id": (C.c_int, [_P]),
     "gck_part_init": (C.c_int, [_P, _P]),
     "gck_part_check": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
@@ -647,6 +649,19 @@ class Engine:
     def part_finish(self, d_perm: int, d_err: int):
         _check(self._lib.gck_part_finish(self._h, d_perm, d_err))
 
+    def part_join_pack(self, d_items: int, n: int, d_send: int, cap_records: int, stream: Optional[int] = None) -> np.ndarray:
+        """gck_part_join_pack: (check, subject slot) records for the owners of the resources,
+        grouped by rank; returns the record count per destination rank."""
+        counts = np.zeros(self.part_world, dtype=np.uint64)
+        _check(self._lib.gck_part_join_pack(self._h, d_items, n, d_send, cap_records,
+                                            counts.ctypes.data_as(C.POINTER(C.c_uint64)), stream))
+        return counts
+
+    def part_join_decide(self, d_items: int, n: int, d_recv: int, n_recv: int, d_perm: int, d_err: int,
+                         stream: Optional[int] = None):
+        """gck_part_join_decide: the received records' checks, decided into perm / err."""
+        _check(self._lib.gck_part_join_decide(self._h, d_items, n, d_recv, n_recv, d_perm, d_err, stream))
+
     @staticmethod
     def part_unique_id() -> bytes:
         """gck_part_unique_id: the RCCL communicator id rank 0 hands to every rank."""
@@ -805,6 +820,7 @@ def _context_arrays(contexts):
 
 
 PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES
+PART_JOIN_RECORD_BYTES = 68  # GCK_PART_JOIN_RECORD_BYTES
 PART_UNIQUE_ID_BYTES = 128  # GCK_PART_UNIQUE_ID_BYTES
 
 

@@ -19,9 +19,10 @@ from typing import Optional, Tuple
 
 import numpy as np
 
-from .engine import PART_ENTRY_BYTES, Engine, part_flag_bytes
+from .engine import PART_ENTRY_BYTES, PART_JOIN_RECORD_BYTES, Engine, part_flag_bytes
 
 _WORDS = PART_ENTRY_BYTES // 4  # an entry is three 32-bit words on the wire
+_RWORDS = PART_JOIN_RECORD_BYTES // 4  # a label-join record (check index, subject slot): 17 words
 
 
 class PartitionedChecker:
@@ -59,7 +60,50 @@ class PartitionedChecker:
 
     def check(self, d_items, n: int, now_us: int = 0) -> Tuple["torch.Tensor", "torch.Tensor"]:
         """``d_items``: a device tensor holding n gck_item records (20 bytes each). Returns
-        (permissionship uint8[n], item error int32[n]) on the device, identical on every rank."""
+        (permissionship uint8[n], item error int32[n]) on the device, identical on every rank.
+        First the label join (one all-to-all of (check, subject slot) records to the owners of
+        the resources, an all-reduce MAX of the decided result bytes), then the level loop over
+        what no rank decided, in batch order."""
+        torch, dist = self.torch, self.dist
+        eng = self.engine
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.cuda else None
+        perm = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        err = torch.zeros(n, dtype=torch.int32, device=self.device)
+        send = torch.empty(max(n, 1) * _RWORDS, dtype=torch.int32, device=self.device)
+        self._sync()
+        counts = eng.part_join_pack(d_items.data_ptr(), n, send.data_ptr(), max(n, 1), stream)
+        send_cnt = torch.from_numpy(counts.astype(np.int64))
+        recv_cnt = torch.zeros(self.world, dtype=torch.int64)
+        if not self.staged:
+            send_cnt, recv_cnt = send_cnt.to(self.device), recv_cnt.to(self.device)
+        dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)
+        rc = recv_cnt.cpu().numpy()
+        n_recv = int(rc.sum())
+        recv = torch.empty(max(n_recv, 1) * _RWORDS, dtype=torch.int32, device=self.device)
+        s_send = self._coll_tensor(send[: int(counts.sum()) * _RWORDS])
+        s_recv = self._coll_tensor(recv[: n_recv * _RWORDS])
+        dist.all_to_all_single(s_recv, s_send, output_split_sizes=[int(c) * _RWORDS for c in rc],
+                               input_split_sizes=[int(c) * _RWORDS for c in counts], group=self.group)
+        self._back(s_recv, recv[: n_recv * _RWORDS])
+        self._sync()
+        eng.part_join_decide(d_items.data_ptr(), n, recv.data_ptr(), n_recv, perm.data_ptr(), err.data_ptr(), stream)
+        f = self._coll_tensor(perm)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+        self._back(f, perm)
+        self._sync()
+        self.joined = int((perm != 0).sum())
+        left = torch.nonzero(perm == 0).flatten()
+        if left.numel() == 0:
+            self.levels = 0
+            return perm, err
+        items2 = d_items.reshape(n, 20)[left].contiguous()
+        p2, e2 = self._loop(items2, int(left.numel()), now_us)
+        perm[left] = p2
+        err[left] = e2
+        return perm, err
+
+    def _loop(self, d_items, n: int, now_us: int = 0):
+        """The level-synchronous loop (gck_part_begin .. gck_part_finish) over d_items."""
         torch, dist = self.torch, self.dist
         eng = self.engine
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.cuda else None

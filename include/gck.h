@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 6
+#define GCK_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -397,7 +397,9 @@ int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resou
  * The caller owns the exchange (RCCL all_to_all / all_reduce over xGMI, or any transport), or
  * gck_part_check runs the loop with RCCL inside libgck (below).
  * Union schemas only (no &, -, all()); check-time caveat contexts are not taken. A partitioned
- * engine refuses gck_check_bulk*. */
+ * engine refuses gck_check_bulk*. A partitioned engine builds its label tables from the rows of its
+ * first snapshot as loaded, before it drops the rows other ranks own; after a Watch batch it runs
+ * without them (every check through the loop). */
 #define GCK_PART_ENTRY_BYTES 12
 #define GCK_PART_FLAG_BYTES(n) (4 * (size_t)(n) + 1)
 /* Before the first snapshot: this engine is rank `rank` of `world` (1 = not partitioned). */
@@ -419,6 +421,22 @@ int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
  * of the begin .. finish sequence; every rank calls it with the same items and gets every
  * result. `stream` orders the batch after the caller's writes of the items (NULL: the legacy
  * default stream). */
+/* The label join over a partitioned graph, before the loop above (labels.inc): the hierarchy
+ * labels are replicated, a subject's slot lives with the subject's owner and a resource's slot
+ * with the resource's owner. gck_part_join_pack writes, for every check whose subject this rank
+ * owns and whose permission has label slots, one GCK_PART_JOIN_RECORD_BYTES record (check index,
+ * the subject's slot) for the owner of the check's resource, grouped by destination rank in rank
+ * order (cap: records); the caller moves them all-to-all (a rank's records for itself included)
+ * and gck_part_join_decide decides the received ones into zero-initialised perm / err arrays. An
+ * all-reduce MAX of the perm bytes then gives every rank every decided check; the checks still at
+ * 0 (undecided: their slots overflowed, another shape, a resource at the depth budget) go through
+ * the begin .. finish loop, in batch order on every rank. gck_part_check does all of it over
+ * RCCL. */
+#define GCK_PART_JOIN_RECORD_BYTES 68
+int gck_part_join_pack(gck_engine* e, const gck_item* d_items, size_t n, void* d_send, size_t send_cap,
+                       uint64_t* send_counts, void* stream);
+int gck_part_join_decide(gck_engine* e, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv,
+                         uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
 #define GCK_PART_UNIQUE_ID_BYTES 128
 int gck_part_unique_id(uint8_t out[GCK_PART_UNIQUE_ID_BYTES]);
 int gck_part_init(gck_engine* e, const uint8_t id[GCK_PART_UNIQUE_ID_BYTES]);

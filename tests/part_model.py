@@ -72,6 +72,14 @@ class ModelRank:
         self.items = items
 
     # ---- protocol ---------------------------------------------------------------------------
+    # the label join (gck_part_join_*): the model has no label tables, so it sends no records and
+    # decides nothing — every check goes through the level loop, as on an engine without them
+    def part_join_pack(self, d_items: int, n: int, d_send: int, cap: int, stream=None) -> np.ndarray:
+        return np.zeros(self.part_world, dtype=np.uint64)
+
+    def part_join_decide(self, d_items: int, n: int, d_recv: int, n_recv: int, d_perm: int, d_err: int, stream=None):
+        assert n_recv == 0
+
     def part_begin(self, d_items: int, n: int, now_us: int = 0, stream=None):
         assert n == len(self.items)
         self.n, self.level = n, 0
