@@ -99,6 +99,9 @@ struct DeviceSnapshot {
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
   bool part_full = false;     // partitioned engine, first snapshot: every row present until part_finish_upload
+  std::vector<uint64_t> lj_key;  // what the label tables were built from (labels.inc: reused while unchanged)
+  std::vector<void*> lj_ptrs;    // their arrays (in allocs or hallocs)
+  uint64_t lj_bytes = 0;
   const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
   uint64_t bytes = 0;
