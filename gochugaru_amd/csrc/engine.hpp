@@ -157,6 +157,7 @@ struct Engine {
   gck_config cfg{};
   int device = 0;
   uint32_t part_rank = 0, part_world = 1;  // partitioned graph (gck_set_partition)
+  bool part_set = false;                   // gck_set_partition was called (any world, one rank too)
   bool device_ready = false;
   std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
   std::unique_ptr<Schema> schema;

@@ -789,6 +789,7 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
             "gck_set_partition must precede the first snapshot");
     e.part_rank = rank;
     e.part_world = world;
+    e.part_set = true;
     if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR;  // both need the whole graph
   });
 }
