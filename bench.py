@@ -370,10 +370,15 @@ def main():
             pc = PartitionedChecker(eng)
         items = torch.cat([WL.checks(args.batch, 1000 + r) for r in range(world)])
         n_global = args.batch * world
-        out = {}
+        out = {"perm": torch.zeros(n_global, dtype=torch.uint8, device=dev),
+               "err": torch.zeros(n_global, dtype=torch.int32, device=dev)}
+        pc_out = (out["perm"], out["err"]) if args.part_backend == "nccl" else None
 
         def step():
-            out["perm"], out["err"] = pc.check(items, n_global)
+            if pc_out is not None:  # (the RCCL checker writes into the preallocated results)
+                pc.check(items, n_global, out=pc_out)
+            else:
+                out["perm"], out["err"] = pc.check(items, n_global)
     elif WL.kind == "mixed":
         # config 5: per step one Watch batch (pre-generated: the stream's arrivals) then one check
         # batch with contexts, at the revision the batch moved the snapshot to

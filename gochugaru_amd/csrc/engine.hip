@@ -2080,17 +2080,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.seq = ++w.pub_seq;
       w.b_seq = j.seq;
     }
-    const dim3 grid((n + 32u * kWaves - 1) / (32u * kWaves)), block(kBlock);
-    hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
-    if (ds.lj_bits == 24 && ds.lj_sw == 16)
-      hipExtLaunchKernelGGL((k_label_join<24, 16>), grid, block, 0, st, e0, e1, 0, j);
-    else if (ds.lj_bits == 24)
-      hipExtLaunchKernelGGL((k_label_join<24, 32>), grid, block, 0, st, e0, e1, 0, j);
-    else if (ds.lj_sw == 16)
-      hipExtLaunchKernelGGL((k_label_join<32, 16>), grid, block, 0, st, e0, e1, 0, j);
-    else
-      hipExtLaunchKernelGGL((k_label_join<32, 32>), grid, block, 0, st, e0, e1, 0, j);
-    HIP_OK(hipGetLastError());
+    lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
   } else if (cj) {
     CjArgs j{};
     j.items = d_items;

@@ -820,7 +820,7 @@ def _context_arrays(contexts):
 
 
 PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES
-PART_JOIN_RECORD_BYTES = 68  # GCK_PART_JOIN_RECORD_BYTES
+PART_JOIN_RECORD_BYTES = 80  # GCK_PART_JOIN_RECORD_BYTES
 PART_UNIQUE_ID_BYTES = 128  # GCK_PART_UNIQUE_ID_BYTES
 
 

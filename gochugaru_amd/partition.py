@@ -22,7 +22,7 @@ import numpy as np
 from .engine import PART_ENTRY_BYTES, PART_JOIN_RECORD_BYTES, Engine, part_flag_bytes
 
 _WORDS = PART_ENTRY_BYTES // 4  # an entry is three 32-bit words on the wire
-_RWORDS = PART_JOIN_RECORD_BYTES // 4  # a label-join record (check index, subject slot): 17 words
+_RWORDS = PART_JOIN_RECORD_BYTES // 4  # a label-join record (check index, 3 reserved, subject slot): 20 words
 
 
 class PartitionedChecker:
@@ -168,12 +168,18 @@ class RcclPartitionedChecker:
         if world > 1:
             dist.broadcast_object_list(box, src=0, group=group)
         engine.part_init(box[0])
+        self._stream = None
 
-    def check(self, d_items, n: int, now_us: int = 0):
+    def check(self, d_items, n: int, now_us: int = 0, out=None):
+        """`out`: (perm uint8[n], err int32[n]) device tensors to write into (a caller's
+        preallocated result buffers); new ones otherwise."""
         torch = self.torch
-        perm = torch.zeros(n, dtype=torch.uint8, device=d_items.device)
-        err = torch.zeros(n, dtype=torch.int32, device=d_items.device)
-        stream = torch.cuda.current_stream(d_items.device).cuda_stream
-        self.engine.part_check(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us, stream)
+        if out is None:
+            out = (torch.zeros(n, dtype=torch.uint8, device=d_items.device),
+                   torch.zeros(n, dtype=torch.int32, device=d_items.device))
+        perm, err = out
+        if self._stream is None:
+            self._stream = torch.cuda.current_stream(d_items.device).cuda_stream
+        self.engine.part_check(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us, self._stream)
         return perm, err
 

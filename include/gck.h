@@ -424,7 +424,7 @@ int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
 /* The label join over a partitioned graph, before the loop above (labels.inc): the hierarchy
  * labels are replicated, a subject's slot lives with the subject's owner and a resource's slot
  * with the resource's owner. gck_part_join_pack writes, for every check whose subject this rank
- * owns and whose permission has label slots, one GCK_PART_JOIN_RECORD_BYTES record (check index,
+ * owns and whose permission has label slots, one GCK_PART_JOIN_RECORD_BYTES record (check index and 3 reserved words,
  * the subject's slot) for the owner of the check's resource, grouped by destination rank in rank
  * order (cap: records); the caller moves them all-to-all (a rank's records for itself included)
  * and gck_part_join_decide decides the received ones into zero-initialised perm / err arrays. An
@@ -432,7 +432,7 @@ int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
  * 0 (undecided: their slots overflowed, another shape, a resource at the depth budget) go through
  * the begin .. finish loop, in batch order on every rank. gck_part_check does all of it over
  * RCCL. */
-#define GCK_PART_JOIN_RECORD_BYTES 68
+#define GCK_PART_JOIN_RECORD_BYTES 80
 int gck_part_join_pack(gck_engine* e, const gck_item* d_items, size_t n, void* d_send, size_t send_cap,
                        uint64_t* send_counts, void* stream);
 int gck_part_join_decide(gck_engine* e, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv,
