@@ -677,9 +677,12 @@ def main():
             tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_batch")
             traffic_src = os.path.relpath(args.traffic_json, os.path.dirname(os.path.abspath(__file__)))
+        # the join stage A ran: the label join (labels.inc) when the snapshot has label tables
+        # and prefers them, else the closure join (closure.inc)
+        kname = "k_label_join" if st_roof.get("label_checks", 0) > 0 else "k_closure_join"
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                "kernel": ("k_closure_join (+ k_bundles<1> over what it leaves): stage A of a batch, timed by the "
+                "kernel": (f"{kname} (+ k_bundles<1> over what it leaves): stage A of a batch, timed by the "
                            "kernel's own start/stop HIP events (hipExtLaunchKernelGGL) on its launch stream, batches "
                            "one at a time after the timed region, submitted as in the timed region (engine streams: "
                            "k_publish follows the join); k_bundles<16> only for deferred giant checks"),
@@ -693,11 +696,11 @@ def main():
                 "engine_streams": bool(args.engine_streams),
                 "launch_timing": "solo" if st_solo is not None else "timed region",
                 "alg_counts": {k: int(v) for k, v in cnt.items()},
-                "mean_launch_ms": {"stage A (k_closure_join + k_bundles<1>)": round(ms_a, 4),
+                "mean_launch_ms": {f"stage A ({kname} + k_bundles<1>)": round(ms_a, 4),
                                    "k_bundles<16>": round(ms_b, 4)},
                 "traffic_source": traffic_src,
                 "note": "latency-bound: a check is two dependent rounds of random 64-B lines (items, then its "
-                        "user and resource slots; closure join); the algorithmic bytes charge the forward BFS "
+                        "user and resource slots; label / closure join); the algorithmic bytes charge the forward BFS "
                         "the engine avoids, so `traffic` (the lines actually moved) is below them; the batches "
                         "in flight overlap, hence achieved_job > achieved; see DESIGN.md"}
 
@@ -812,7 +815,8 @@ def main():
                        "giant_ms_per_batch": round(st["giant_ms"] / n_batches, 4),
                        "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2),
                        "closure_checks_per_batch": round(st["closure_checks"] / n_batches, 1),
-                       "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1)},
+                       "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1),
+                       "label_checks_per_batch": round(st["label_checks"] / n_batches, 1)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
             **({"caveats": {"evals_per_step": round(st["caveat_evals"] / args.steps, 1),
                             "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}

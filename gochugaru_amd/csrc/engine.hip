@@ -137,6 +137,7 @@ struct Workspace {
   uint8_t* b_xperm = nullptr; // host batch: where the results' D2H lands — the pinned staging, or
   int32_t* b_xerr = nullptr;  // the caller's buffers themselves when they are gck_host_alloc memory
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
+  bool b_label = false;       // ... and it was the label join
   bool b_closure = false;     // stage A began with the closure join: its leftovers are bundled in finish
   bool b_chained = false;     // ... or already in stage A, by bundles chained on the device
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
@@ -1277,6 +1278,11 @@ void device_free(Engine& e) {
     e.delta_scratch = nullptr;
     e.delta_scratch_cap = 0;
   }
+  if (e.delta_host) {
+    (void)hipHostFree(e.delta_host);
+    e.delta_host = nullptr;
+    e.delta_host_cap = 0;
+  }
   if (e.dev) {
     (void)hipSetDevice(e.device);
     free_list(e.dev->allocs);
@@ -2052,6 +2058,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   const bool lj = ds.d_lj && (!cj_ok || ds.lj_preferred);
   const bool cj = cj_ok && !lj;
   w.b_closure = cj || lj;
+  w.b_label = lj;
   // chained: the wave bundles over the join's deferred list follow it in stage A, reading the
   // list's length on the device — no host round trip in the wait — when recent batches of the
   // engine left checks (a persistent bundle launch over an empty list costs a few microseconds,
@@ -2173,6 +2180,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     std::lock_guard<std::mutex> lk(e.stats_mu);
     e.stats.closure_checks += n - n_cj;
     e.stats.slot_checks += n - n_cj - tasks;
+    if (w.b_label) e.stats.label_checks += n - n_cj;
   }
   // recent batches with leftovers make the next ones chain their bundles on the device
   if (w.b_closure) {

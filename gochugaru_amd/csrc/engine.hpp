@@ -198,6 +198,8 @@ struct Engine {
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
   size_t delta_scratch_cap = 0;
+  void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
+  size_t delta_host_cap = 0;
   gck_stats stats{};
   // batches to come that chain the wave bundles behind the join in stage A (engine.hip
   // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 7
+#define GCK_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -220,6 +220,8 @@ typedef struct gck_stats {
   uint64_t caveat_passes;      /* extra batch passes after lazily evaluated caveat pairs */
   uint64_t slot_checks;        /* checks the closure join decided from their user / resource slots
                                   alone (one read each) */
+  uint64_t label_checks;       /* of closure_checks: those the label join (labels.inc k_label_join,
+                                  or its partitioned form) answered */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

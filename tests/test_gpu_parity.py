@@ -232,6 +232,7 @@ def test_random_parity(family, seed, path):
         assert e.stats()["slot_checks"] == 0
     if path == "labels" and family in ("nested", "gdocs", "github", "gdocs_deep"):
         assert e.stats()["slot_checks"] > 0  # decided by the label join's slots
+        assert e.stats()["label_checks"] > 0
     if path == "noclosure" and family in ("nested", "gdocs_deep"):
         assert e.stats()["bidir_checks"] > 0 and e.stats()["closure_checks"] == 0
     if path in ("nobidir", "wide") or family == "caveated":

@@ -1,32 +1,41 @@
-"""Per-batch timeline of a rocprofv3 kernel trace (kernel_trace.csv): per kernel name its mean
-duration, and the mean gap from the previous kernel's end on the same queue."""
+"""Timeline of the last --last batches of a rocprofv3 kernel trace (the timed region of a bench.py
+run with --no-profile --host-steps 0 --no-oracle, whose final launches are the timed batches):
+per engine kernel launch its start / end relative to the first one, duration and queue, and the
+span of the whole group, so that fill / drain and gaps between batches can be read off.
+
+    python tools/trace_gaps.py <kernel_trace.csv> [--last 20] [--kernel k_label_join]
+"""
+import argparse
 import csv
-import glob
-import sys
-from collections import defaultdict
+import json
 
 
-def short(n):
-    for k in ("k_closure_join", "k_bundles<1,", "k_bundles<16,", "k_publish", "k_gather", "k_scatter"):
-        if k in n:
-            return k.rstrip("<,")
-    return n[:40]
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--last", type=int, default=20)
+    ap.add_argument("--kernel", default="k_label_join")
+    args = ap.parse_args()
+    rows = [r for r in csv.DictReader(open(args.trace)) if "gck::" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    heads = [i for i, r in enumerate(rows) if args.kernel in r["Kernel_Name"]]
+    if not heads:
+        print(json.dumps({"error": f"no {args.kernel} launches"}))
+        return
+    first = heads[-args.last] if len(heads) >= args.last else heads[0]
+    sel = rows[first:]
+    t0 = int(sel[0]["Start_Timestamp"])
+    out = []
+    for r in sel:
+        s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("gck::", "")
+        out.append({"k": name, "start_us": round(s / 1e3, 2), "end_us": round(e / 1e3, 2),
+                    "dur_us": round((e - s) / 1e3, 2), "queue": r.get("Queue_Id"), "stream": r.get("Stream_Id")})
+    span = max(o["end_us"] for o in out)
+    busy = sum(o["dur_us"] for o in out if args.kernel in o["k"])
+    print(json.dumps({"launches": len(out), "span_us": span, f"{args.kernel}_sum_us": round(busy, 2),
+                      "timeline": out}, indent=0))
 
 
-rows = []
-for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r.get("Queue_Id", "0")))
-rows.sort()
-dur, gap, cnt = defaultdict(float), defaultdict(float), defaultdict(int)
-last_end = {}
-for s, e, k, q in rows:
-    dur[k] += e - s
-    cnt[k] += 1
-    if q in last_end:
-        gap[k] += max(0, s - last_end[q])
-    last_end[q] = e
-span = (rows[-1][1] - rows[0][0]) / 1e3 if rows else 0
-print(f"kernels={len(rows)} span_us={span:.1f}")
-for k in sorted(cnt, key=lambda x: -dur[x]):
-    print(f"{k:20s} n={cnt[k]:6d} mean_dur_us={dur[k] / cnt[k] / 1e3:8.2f} mean_gap_before_us={gap[k] / cnt[k] / 1e3:8.2f}")
+if __name__ == "__main__":
+    main()
