@@ -386,9 +386,14 @@ def main():
         items = WL.checks(args.batch, 1000 + rank)
         perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
         err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+        # The check batch is submitted and left running: the next step's Watch batch validates,
+        # groups and stages its updates beside it and drains it before it touches the snapshot
+        # (delta.inc device_apply), so every check batch runs on the revision its step applied
+        from gochugaru_amd.engine import Contexts
         n_up = max(1, int(n_tuples * args.churn))
         batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warm + args.steps)]
-        rev = {"r": 1, "k": 0, "apply_s": 0.0}
+        rev = {"r": 1, "k": 0, "apply_s": 0.0, "pending": None}
+        m_ctx = Contexts(CONTEXTS)
 
         def step():
             t_a = time.perf_counter()
@@ -396,8 +401,16 @@ def main():
             eng.apply_updates(rev["r"], batches[rev["k"]])
             rev["k"] += 1
             rev["apply_s"] += time.perf_counter() - t_a
-            eng.check_bulk_device(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), stream=stream,
-                                  contexts=CONTEXTS)
+            b = eng.submit(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), device=True,
+                           stream=stream, contexts=m_ctx)
+            if rev["pending"] is not None:
+                rev["pending"].wait()  # (already finished by the apply above)
+            rev["pending"] = b
+
+        def drain():
+            if rev["pending"] is not None:
+                rev["pending"].wait()
+                rev["pending"] = None
     elif WL.kind == "quota":
         # per step one batch with its own 64K contexts (pre-generated, rotated): the contexts are
         # parsed, the walk records the (instance, context) pairs it meets, the host evaluates
@@ -472,7 +485,7 @@ def main():
     else:
         for _ in range(args.warm):
             step()
-    if WL.kind not in ("mixed", "quota") and not args.partitioned:
+    if WL.kind != "quota" and not args.partitioned:
         drain()
     torch.cuda.synchronize()
     eng.reset_stats()
@@ -485,7 +498,7 @@ def main():
     else:
         for _ in range(args.steps):
             step()
-    if WL.kind not in ("mixed", "quota") and not args.partitioned:
+    if WL.kind != "quota" and not args.partitioned:
         drain()
     torch.cuda.synchronize()
     if world > 1:

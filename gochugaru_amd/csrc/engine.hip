@@ -1575,19 +1575,24 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     // own non-blocking stream, where a free costs a fraction of one on the legacy null stream,
     // which must order itself after every blocking stream
     static const bool null_free = getenv("GCK_FREE_NULL") != nullptr;  // A/B
+    const size_t n_free = e.dev->allocs.size();
     if (e.free_stream && !null_free) {
       for (void* p : e.dev->allocs) (void)hipFreeAsync(p, (hipStream_t)e.free_stream);
       e.dev->allocs.clear();
     } else {
       free_list(e.dev->allocs);
     }
+    pc.mark(n_free > 16 ? "free_many" : "free_few");
     for (void* p : e.dev->hallocs) (void)hipFree(p);
+    pc.mark(e.dev->hallocs.empty() ? "free_h0" : "free_h");
     delete e.dev;
   }
+  pc.mark("retire");
   e.dev = ds;
   static std::atomic<uint64_t> g_generations{0};  // process-wide: a snapshot id never repeats
   e.generation = ++g_generations;
   HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
+  pc.mark("sync");
 }
 
 // ---- workspaces ------------------------------------------------------------------------------

@@ -200,6 +200,7 @@ struct Engine {
   size_t delta_scratch_cap = 0;
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
+  std::vector<uint64_t> group_scratch;  // group_updates' sort buffers, kept across Watch batches
   gck_stats stats{};
   // batches to come that chain the wave bundles behind the join in stage A (engine.hip
   // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none
@@ -229,7 +230,7 @@ void load_snapshot_file(Engine& e, const std::string& path);
 std::vector<HostCSR> build_csrs(Engine& e);
 // Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
 void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
-std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>& ups);
+std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n);
 
 // engine.hip
 int device_init(Engine& e);

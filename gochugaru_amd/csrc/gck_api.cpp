@@ -486,21 +486,22 @@ int gck_device_bytes(gck_engine* ge, uint64_t* out) {
 
 // Watch batch: validated and grouped on the host first (nothing is applied if any update is
 // rejected), then merged on the device (delta.inc). A device failure loses the snapshot.
-static void apply_updates(Engine& e, uint64_t revision, const std::vector<gck_update>& ups) {
+static void apply_updates(Engine& e, uint64_t revision, const gck_update* ups, size_t n) {
   REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
-  REQUIRE(revision > e.revision || (ups.empty() && revision == e.revision), GCK_E_REVISION,
+  REQUIRE(revision > e.revision || (n == 0 && revision == e.revision), GCK_E_REVISION,
           "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
               std::to_string(e.revision));
-  std::vector<gck_update> mine;
-  const std::vector<gck_update>* use = &ups;
-  if (e.part_world > 1) {  // partitioned graph: this rank keeps the rows it owns
-    for (const gck_update& u : ups)
-      if (part_owner(u.tuple.resource_id, e.part_world) == e.part_rank) mine.push_back(u);
-    use = &mine;
-  }
   PhaseClock pc("watch");
-  std::vector<UpdateGroup> groups = group_updates(e, *use);
+  std::vector<gck_update> mine;
+  if (e.part_world > 1) {  // partitioned graph: this rank keeps the rows it owns
+    for (size_t i = 0; i < n; ++i)
+      if (part_owner(ups[i].tuple.resource_id, e.part_world) == e.part_rank) mine.push_back(ups[i]);
+    ups = mine.data();
+    n = mine.size();
+  }
+  std::vector<UpdateGroup> groups = group_updates(e, ups, n);
   pc.mark("group");
+  if (groups.empty()) drain_batches(e);  // (device_apply drains otherwise)
   if (!groups.empty()) {
     try {
       device_apply(e, groups);
@@ -519,8 +520,9 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
     need_schema(e);
     REQUIRE(n == 0 || updates, GCK_E_INVALID_ARGUMENT, "null updates");
     std::unique_lock<std::shared_mutex> lk(e.mu);
-    drain_batches(e);
-    apply_updates(e, revision, std::vector<gck_update>(updates, updates + n));
+    // (read in place: no copy of the batch). Batches in flight are drained once the updates are
+    // validated, grouped and staged (delta.inc device_apply): that host work runs beside them
+    apply_updates(e, revision, updates, n);
   });
 }
 
@@ -578,7 +580,7 @@ int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, 
     try {
       std::vector<gck_update> ups;
       parse_updates_text(e, text, len, ups);
-      apply_updates(e, revision, ups);
+      apply_updates(e, revision, ups.data(), ups.size());
     } catch (...) {
       intern_rollback(e, mark);
       throw;

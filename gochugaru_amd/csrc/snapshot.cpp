@@ -327,60 +327,129 @@ void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck
 }
 
 // Validates the updates and groups them per (relation, subject type, subject relation); within a
-// group the last write per (object, subject) wins (the order of the Watch stream).
-std::vector<UpdateGroup> group_updates(Engine& e, const std::vector<gck_update>& ups) {
-  struct U {
-    uint16_t rel, stype, srel;
-    uint32_t obj, sid, cav;
-    int64_t exp_us;
-    uint32_t op;
-    size_t seq;
+// group the last write per (object, subject) wins (the order of the Watch stream). Groups come
+// out in ascending (relation, subject type, subject relation) order, keys ascending: a stable
+// counting pass into the groups (a batch touches a few kinds), then per group a stable LSD radix
+// sort of the 64-bit (object << 32 | subject) keys in 11-bit digits, digits constant over the
+// group skipped (a comparison sort of a 10K-update batch cost ~0.2 ms of the Watch step).
+std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n) {
+  PhaseClock pc("group");
+  const Schema& sc = *e.schema;
+  // scratch kept by the engine (a Watch batch holds it exclusively): per update its kind index,
+  // then two (key, index) buffers for the radix passes — no allocation or clearing per batch
+  std::vector<uint64_t>& scr = e.group_scratch;
+  if (scr.size() < 5 * n) scr.resize(5 * n);
+  uint32_t* g_of = reinterpret_cast<uint32_t*>(scr.data());
+  struct KI {
+    uint64_t k;  // (object << 32) | subject
+    uint64_t i;  // update index << 34 | upsert << 33 | has expiration << 32 | caveat
   };
-  std::vector<U> v;
-  v.reserve(ups.size());
-  for (size_t i = 0; i < ups.size(); ++i) {
+  KI* a = reinterpret_cast<KI*>(scr.data() + n);
+  KI* b = reinterpret_cast<KI*>(scr.data() + 3 * n);
+  std::vector<uint64_t> kinds;  // distinct (relation, subject type, subject relation)
+  // (resource type, kind, wildcard subject) combinations whose schema checks passed: the checks
+  // depend on nothing else, so each is made once per batch
+  std::vector<uint64_t> seen;
+  std::vector<uint32_t> seen_g;
+  if (n >= (1ull << 30)) throw Error(GCK_E_CAPACITY, "a Watch batch holds at most 2^30 updates");
+  for (size_t i = 0; i < n; ++i) {
     const gck_update& u = ups[i];
     if (u.op != GCK_UPDATE_CREATE && u.op != GCK_UPDATE_TOUCH && u.op != GCK_UPDATE_DELETE)
       throw Error(GCK_E_INVALID_ARGUMENT, "unknown update operation " + std::to_string(u.op));
-    validate_tuple(e, u.tuple);
     const gck_tuple& t = u.tuple;
-    v.push_back({t.relation, t.subject_type, t.subject_relation, t.resource_id, t.subject_id, t.caveat,
-                 t.expires_at_us, u.op, i});
-  }
-  // one 64-bit kind key (relation, subject type, subject relation) and one 64-bit (object,
-  // subject) key per update, sorted as a pair of indices: two integer compares per step instead of
-  // six fields (a Watch batch of ~10K updates sorts in a few tens of microseconds)
-  std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> order(v.size());
-  for (size_t i = 0; i < v.size(); ++i)
-    order[i] = {{((uint64_t)v[i].rel << 32) | ((uint64_t)v[i].stype << 16) | v[i].srel,
-                 ((uint64_t)v[i].obj << 32) | v[i].sid},
-                (uint32_t)i};  // index == seq: equal keys stay in arrival order
-  std::sort(order.begin(), order.end());
-  {
-    std::vector<U> w(v.size());
-    for (size_t i = 0; i < v.size(); ++i) w[i] = v[order[i].second];
-    v.swap(w);
-  }
-  std::vector<UpdateGroup> out;
-  for (size_t i = 0; i < v.size(); ++i) {
-    const U& x = v[i];
-    if (i + 1 < v.size() && v[i + 1].rel == x.rel && v[i + 1].stype == x.stype && v[i + 1].srel == x.srel &&
-        v[i + 1].obj == x.obj && v[i + 1].sid == x.sid)
-      continue;  // a later write of the same relationship follows
-    if (out.empty() || out.back().rel != x.rel || out.back().stype != x.stype || out.back().srel != x.srel) {
-      out.emplace_back();
-      out.back().rel = x.rel;
-      out.back().stype = x.stype;
-      out.back().srel = x.srel;
+    const uint64_t combo = ((uint64_t)(t.resource_type & 0x7FFF) << 48) | ((uint64_t)t.relation << 32) |
+                           ((uint64_t)t.subject_type << 16) | t.subject_relation |
+                           (t.subject_id == kWildcard ? (1ull << 63) : 0ull);
+    size_t c = 0;
+    while (c < seen.size() && seen[c] != combo) ++c;
+    if (c == seen.size()) {
+      validate_tuple(e, t);
+      const uint64_t gk = combo & 0xFFFFFFFFFFFFull;
+      size_t j = 0;
+      while (j < kinds.size() && kinds[j] != gk) ++j;
+      if (j == kinds.size()) kinds.push_back(gk);
+      seen.push_back(combo);
+      seen_g.push_back((uint32_t)j);
+    } else if (t.resource_id >= e.interner[t.resource_type].count ||
+               (t.subject_id != kWildcard && t.subject_id >= e.interner[t.subject_type].count) ||
+               t.caveat >= e.caveat_instances.size()) {
+      validate_tuple(e, t);  // (raises the error)
     }
-    UpdateGroup& g = out.back();
-    g.keys.push_back(((unsigned long long)x.obj << 32) | x.sid);
-    const bool up = x.op != GCK_UPDATE_DELETE;
-    g.upsert.push_back(up ? 1 : 0);
-    g.is_ext.push_back(up && (x.cav != 0 || x.exp_us != 0) ? 1 : 0);
-    g.cav.push_back(up ? x.cav : 0);
-    g.exp_us.push_back(up ? x.exp_us : 0);
+    g_of[i] = seen_g[c];
   }
+  (void)sc;
+  pc.mark("validate");
+  const size_t G = kinds.size();
+  std::vector<uint32_t> by_kind(G), rank(G);
+  for (size_t j = 0; j < G; ++j) by_kind[j] = (uint32_t)j;
+  std::sort(by_kind.begin(), by_kind.end(), [&](uint32_t x, uint32_t y) { return kinds[x] < kinds[y]; });
+  for (size_t j = 0; j < G; ++j) rank[by_kind[j]] = (uint32_t)j;
+  std::vector<size_t> start(G + 1, 0);
+  for (size_t i = 0; i < n; ++i) ++start[rank[g_of[i]] + 1];
+  for (size_t j = 0; j < G; ++j) start[j + 1] += start[j];
+  {
+    std::vector<size_t> at(start.begin(), start.end() - 1);
+    // the sort records carry what the groups need (upsert, expiration present, caveat) next to
+    // the update's index, so that only updates with an expiration are read again
+    for (size_t i = 0; i < n; ++i) {
+      const gck_tuple& t = ups[i].tuple;
+      const uint64_t up = ups[i].op != GCK_UPDATE_DELETE ? 1 : 0;
+      a[at[rank[g_of[i]]]++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
+                                ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) |
+                                    t.caveat};
+    }
+  }
+  pc.mark("scatter");
+  std::vector<UpdateGroup> out(G);
+  uint32_t cnt[2049];
+  for (size_t gi = 0; gi < G; ++gi) {
+    const size_t lo = start[gi], hi = start[gi + 1];
+    uint64_t orv = 0, andv = ~0ull;
+    for (size_t i = lo; i < hi; ++i) {
+      orv |= a[i].k;
+      andv &= a[i].k;
+    }
+    KI* src = a;
+    KI* dst = b;
+    for (int sh = 0; sh < 64; sh += 11) {
+      if ((((orv ^ andv) >> sh) & 2047) == 0) continue;  // constant digit
+      std::memset(cnt, 0, sizeof cnt);
+      for (size_t i = lo; i < hi; ++i) ++cnt[((src[i].k >> sh) & 2047) + 1];
+      for (int j = 0; j < 2048; ++j) cnt[j + 1] += cnt[j];
+      for (size_t i = lo; i < hi; ++i) dst[lo + cnt[(src[i].k >> sh) & 2047]++] = src[i];
+      std::swap(src, dst);
+    }
+    const uint64_t kind = kinds[by_kind[gi]];
+    UpdateGroup& g = out[gi];
+    g.rel = (uint16_t)(kind >> 32);
+    g.stype = (uint16_t)(kind >> 16);
+    g.srel = (uint16_t)kind;
+    const size_t m = hi - lo;
+    g.keys.resize(m);
+    g.upsert.resize(m);
+    g.is_ext.resize(m);
+    g.cav.resize(m);
+    g.exp_us.resize(m);
+    size_t w = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      if (i + 1 < hi && src[i + 1].k == src[i].k) continue;  // a later write of the same relationship follows
+      const uint64_t v = src[i].i;
+      const bool up = (v >> 33) & 1, has_exp = (v >> 32) & 1;
+      const uint32_t cav = (uint32_t)v;
+      g.keys[w] = src[i].k;
+      g.upsert[w] = up ? 1 : 0;
+      g.is_ext[w] = up && (cav != 0 || has_exp) ? 1 : 0;
+      g.cav[w] = up ? cav : 0;
+      g.exp_us[w] = up && has_exp ? ups[v >> 34].tuple.expires_at_us : 0;
+      ++w;
+    }
+    g.keys.resize(w);
+    g.upsert.resize(w);
+    g.is_ext.resize(w);
+    g.cav.resize(w);
+    g.exp_us.resize(w);
+  }
+  pc.mark("sort");
   return out;
 }
 
