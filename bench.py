@@ -58,6 +58,8 @@ def parse():
                          "kernels fill the tail of the previous one; 1 = one batch at a time (default: 8 for "
                          "config 4, 3 for the others)")
     ap.add_argument("--no-profile", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--trace-loop", action="store_true",
+                    help="record when each timed batch's submit and wait returned (compiled loop; `loop_trace`)")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="who runs the submit/wait loop over the device batches: native = the compiled loop "
                          "of libgck_driver.so (what a cgo caller runs), python = one ctypes call per submit/wait")
@@ -350,6 +352,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev).cuda_stream
     run_steps = None  # the nested workload's compiled submit/wait loop (--driver native)
+    loop_s = {"s": None}  # the compiled loop's own wall time of the last phase (first submit to last wait)
     if args.partitioned:
         # one global batch: every rank's 64K checks, the same items on every rank
         from gochugaru_amd.partition import PartitionedChecker, RcclPartitionedChecker
@@ -474,7 +477,7 @@ def main():
                 c, run = prepared.pop(min(prepared))
                 assert c == count
                 cursor["k"] += count
-                run.run()
+                loop_s["s"] = run.run()
 
             prepare(args.warm)
             prepare(args.steps)
@@ -492,6 +495,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    trace = None
+    if native and args.trace_loop:  # per-batch submit / wait return times of the timed loop
+        from gochugaru_amd.engine import _driver
+        import ctypes
+        trace = np.zeros(2 * args.steps, dtype=np.float64)
+        _driver().gckd_set_trace(trace.ctypes.data_as(ctypes.c_void_p), args.steps)
     t0 = time.perf_counter()
     if native:
         run_steps(args.steps)
@@ -504,7 +513,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms")
+    if trace is not None:
+        _driver().gckd_set_trace(None, 0)
+    progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms"
+             + (f" (compiled loop {loop_s['s'] * 1e3:.3f} ms)" if native else ""))
     if WL.kind not in ("mixed", "quota") and not args.partitioned:  # the first timed batch and its results
         items, (perm, err) = rot[args.warm], outs[args.warm]
     if WL.kind == "quota":
@@ -831,6 +843,10 @@ def main():
                        "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1),
                        "label_checks_per_batch": round(st["label_checks"] / n_batches, 1)},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
+            **({"timed_loop_ms": round(loop_s["s"] * 1e3, 4)} if loop_s["s"] is not None else {}),
+            **({"loop_trace_us": {"submit_returned": [round(x * 1e6, 1) for x in trace[0::2]],
+                                  "wait_returned": [round(x * 1e6, 1) for x in trace[1::2]]}}
+               if trace is not None else {}),
             **({"caveats": {"evals_per_step": round(st["caveat_evals"] / args.steps, 1),
                             "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}
                if WL.kind == "quota" else {}),

@@ -15,7 +15,21 @@ using submit_fn = int (*)(gck_engine*, const gck_consistency*, const gck_item*, 
                           const size_t*, size_t, int64_t, uint8_t*, int32_t*, uint32_t, void*, gck_batch**);
 using wait_fn = int (*)(gck_engine*, gck_batch*);
 
+// Optional per-batch timeline of the next loops (gckd_set_trace): for batch k, the seconds after
+// the loop's start at which its submit and its wait returned (stamps[2k], stamps[2k + 1]).
+static double* g_stamps = nullptr;
+static size_t g_cap = 0;
+
 extern "C" {
+
+static inline void stamp(std::chrono::steady_clock::time_point t0, size_t k, int which) {
+  if (k < g_cap) g_stamps[2 * k + which] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void gckd_set_trace(double* stamps, size_t n_batches) {
+  g_stamps = stamps;
+  g_cap = stamps ? n_batches : 0;
+}
 
 // Runs batches k = 0 .. n_batches-1 (device buffers items[k], perm[k], err[k], n checks each) with
 // up to `depth` in flight; batch k is submitted on streams[k % depth] with GCK_SUBMIT_DEVICE | flags
@@ -31,6 +45,7 @@ int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistenc
   for (size_t k = 0; k < n_batches && rc == GCK_OK; ++k) {
     if (q.size() >= depth) {
       rc = wait(e, q.front());
+      stamp(t0, k - depth, 1);
       q.pop_front();
       if (rc != GCK_OK) break;
     }
@@ -39,9 +54,12 @@ int gckd_run(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consistenc
                 reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), GCK_SUBMIT_DEVICE | flags,
                 reinterpret_cast<void*>(streams[k % depth]), &b);
     if (rc == GCK_OK) q.push_back(b);
+    stamp(t0, k, 0);
   }
+  size_t kw = n_batches - q.size();
   while (!q.empty()) {  // every submitted batch is waited for, also after an error
     const int r = wait(e, q.front());
+    stamp(t0, kw++, 1);
     if (rc == GCK_OK) rc = r;
     q.pop_front();
   }
@@ -62,6 +80,7 @@ int gckd_run_host(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consi
   for (size_t k = 0; k < n_batches && rc == GCK_OK; ++k) {
     if (q.size() >= depth) {
       rc = wait(e, q.front());
+      stamp(t0, k - depth, 1);
       q.pop_front();
       if (rc != GCK_OK) break;
     }
@@ -69,9 +88,12 @@ int gckd_run_host(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consi
     rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, now_us,
                 reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), 0u, nullptr, &b);
     if (rc == GCK_OK) q.push_back(b);
+    stamp(t0, k, 0);
   }
+  size_t kw = n_batches - q.size();
   while (!q.empty()) {
     const int r = wait(e, q.front());
+    stamp(t0, kw++, 1);
     if (rc == GCK_OK) rc = r;
     q.pop_front();
   }

@@ -408,6 +408,17 @@ template <class T>
 __device__ __forceinline__ GCK_GLOBAL T* gptr_w(T* p) {
   return (GCK_GLOBAL T*)p;
 }
+// A result of a batch the join publishes before its kernel has ended, on a stream no reader is
+// ordered after (GCK_SUBMIT_ENGINE_STREAM): an agent-scope store, written through the XCD's L2, so
+// that once the wave's stores have completed (s_waitcnt) the value is visible to every XCD and
+// to the copy engines — no end-of-kernel L2 write-back is needed before the publication.
+template <class T>
+__device__ __forceinline__ void store_result(T* p, T v, bool coherent) {
+  if (coherent)
+    __hip_atomic_store(gptr_w(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *gptr_w(p) = v;
+}
 __device__ __forceinline__ uint32_t csr_off(const DevCSR& r, uint32_t i) { return gptr(r.off)[i]; }
 __device__ __forceinline__ uint32_t csr_nbr(const DevCSR& r, uint32_t p) { return gptr(r.nbr)[p]; }
 __device__ __forceinline__ uint32_t csr_cav(const DevCSR& r, uint32_t p) { return gptr(r.cav)[p]; }
@@ -2069,7 +2080,16 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // engine left checks (a persistent bundle launch over an empty list costs a few microseconds,
   // the round trip tens; engine.hpp Engine::defer_recent)
   w.b_chained = w.b_closure && e.defer_recent.load(std::memory_order_relaxed) > 0;
-  const bool self_pub = !host_out && !w.b_own_stream && !w.b_chained;
+  // the join publishes the batch itself unless something must follow it first: a host batch's
+  // copies, the chained bundles, or — for a device batch on the engine's stream, whose caller has
+  // no stream to order its reads after the kernel's end — the end-of-kernel L2 write-back
+  // (k_publish after the join). GCK_COHERENT_PUBLISH=1 publishes those from the join too, with
+  // the results written through the L2 (store_result, `coherent`): measured slower (config 4, 8
+  // in flight: 9.2 vs 10.3 G checks/s; solo stage A 16.1 vs 12.3 us — every wave waits for its
+  // write-through acks before its block arrives), so off by default.
+  static const bool coherent_pub = getenv("GCK_COHERENT_PUBLISH") && atoi(getenv("GCK_COHERENT_PUBLISH")) != 0;
+  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub);
+  const uint32_t coherent = w.b_own_stream ? 1u : 0u;
   if (lj) {
     // the label join (labels.inc): one round of slot lines per check; what it leaves goes to the
     // wave bundles through the same deferred list as the closure join's
@@ -2090,6 +2110,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.h_out = w.d_hpub;
       j.done = w.b_ctrs + kBDone;
       j.seq = ++w.pub_seq;
+      j.coherent = coherent;
       w.b_seq = j.seq;
     }
     lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
@@ -2109,17 +2130,15 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
     j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
-    // the join publishes the batch itself, unless something must follow it first: a host batch's
-    // copies, or — for a device batch on the engine's stream, whose caller has no stream to order
-    // its reads — the join's end (k_publish after it sees every block's results written back
-    // past the L2s; the join's own last block sees only that every block has decided: a host-side
-    // stream query or synchronisation per batch instead costs ~10 us, 11 G -> 3-5 G checks/s)
+    // self-published as the label join (a host-side stream query or synchronisation per batch
+    // instead costs ~10 us, 11 G -> 3-5 G checks/s)
     if (self_pub) {
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
       j.h_out = w.d_hpub;
       j.done = w.b_ctrs + kBDone;
       j.seq = ++w.pub_seq;
+      j.coherent = coherent;
       w.b_seq = j.seq;
     }
     // a timed batch's events are the kernel's own start and stop (hipExtLaunchKernel), not markers

@@ -223,6 +223,8 @@ def _driver():
         d.gckd_run_host.restype = C.c_int
         d.gckd_run_host.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_size_t, C.c_uint32, C.c_int64, C.POINTER(C.c_double)]
+        d.gckd_set_trace.restype = None
+        d.gckd_set_trace.argtypes = [C.c_void_p, C.c_size_t]
         _DRIVER = d
     return _DRIVER
 

@@ -277,6 +277,46 @@ def test_compiled_submit_loop(engine_streams):
     e.close()
 
 
+@pytest.mark.parametrize("family", ["nested", "gdocs"])
+def test_engine_stream_results_read_right_after_wait(family):
+    """A device batch on the engine's stream has no caller stream to order reads after: the
+    results a caller reads on another stream the moment gck_check_wait returns — no
+    synchronisation with the engine's stream — are the final ones (k_publish after the join, or,
+    under GCK_COHERENT_PUBLISH=1, write-through results published by the join's last block).
+    48 batches over poisoned buffers, 3 in flight."""
+    import torch
+    schema, tuples, checks = getattr(gen, family)(3)
+    e = _engine(schema, tuples, workspaces=3)
+    want = _want(schema, tuples, checks)
+    items = e.make_items([parse_check(c) for c in checks])
+    n = len(items)
+    d_items = [torch.from_numpy(np.roll(items, k).view(np.uint8).copy()).cuda() for k in range(8)]
+    reader = torch.cuda.Stream()
+    for rnd in range(6):
+        outs = [(torch.full((n,), 0xFF, dtype=torch.uint8, device="cuda"),
+                 torch.full((n,), -7, dtype=torch.int32, device="cuda")) for _ in range(8)]
+        torch.cuda.synchronize()
+        pending, copies = [], {}
+        for k in range(8):
+            if len(pending) >= 3:
+                j, b = pending.pop(0)
+                b.wait()
+                with torch.cuda.stream(reader):  # read at once, on a stream the engine never saw
+                    copies[j] = (outs[j][0].clone(), outs[j][1].clone())
+            pending.append((k, e.submit(d_items[k].data_ptr(), n, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
+                                        now_us=gen.NOW_US, device=True, engine_stream=True)))
+        for j, b in pending:
+            b.wait()
+            with torch.cuda.stream(reader):
+                copies[j] = (outs[j][0].clone(), outs[j][1].clone())
+        reader.synchronize()
+        for k in range(8):
+            rolled = (want[-k:] + want[:-k]) if k else want
+            assert _got(copies[k][0].cpu().numpy(), copies[k][1].cpu().numpy()) == rolled, (rnd, k)
+    torch.cuda.synchronize()
+    e.close()
+
+
 def test_no_allocation_after_commit():
     """Every workspace exists once the snapshot is committed (engine.hip ensure_pool): the first
     batches after the commit — as many concurrent ones as the pool holds — allocate nothing, so
