@@ -841,7 +841,8 @@ def main():
                        "deferred_wide_per_batch": round(st["deferred_wide"] / n_batches, 2),
                        "closure_checks_per_batch": round(st["closure_checks"] / n_batches, 1),
                        "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1),
-                       "label_checks_per_batch": round(st["label_checks"] / n_batches, 1)},
+                       "label_checks_per_batch": round(st["label_checks"] / n_batches, 1),
+                       "aql_dispatched_batches": int(st["aql_batches"])},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
             **({"timed_loop_ms": round(loop_s["s"] * 1e3, 4)} if loop_s["s"] is not None else {}),
             **({"loop_trace_us": {"submit_returned": [round(x * 1e6, 1) for x in trace[0::2]],

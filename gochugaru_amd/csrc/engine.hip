@@ -19,8 +19,12 @@
 //
 // Every frontier level is one dispatch wave of SpiceDB's recursion, so the depth budget
 // (max_depth, default 50) is enforced per entry exactly as dispatch.CheckDepth does.
+#include <cxxabi.h>
+#include <dlfcn.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -30,6 +34,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -142,6 +148,10 @@ struct Workspace {
   bool b_chained = false;     // ... or already in stage A, by bundles chained on the device
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
+  bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
+  void* aql_kernarg = nullptr;  // aql.inc: pinned kernarg block of the dispatched join
+  uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
+  void* aql_queue = nullptr;    // aql.inc: the engine queue this workspace dispatches into
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
   unsigned b_seq = 0;         // publish sequence of stage A
   float b_ms = 0.f;
@@ -1263,8 +1273,11 @@ struct CsrInfo;
 static void part_finish_upload(Engine& e, DeviceSnapshot& ds, std::vector<DevNode>& nodes, std::vector<DevCSR>& table,
                                std::vector<CsrInfo>& info, const std::vector<size_t>& later);
 
+static void aql_workspace_free(Workspace& w);  // aql.inc
+
 static void free_workspace(Workspace* w) {
   if (w->stream) (void)hipStreamSynchronize(w->stream);
+  aql_workspace_free(*w);
   if (w->b_st && w->state == 1) (void)hipStreamSynchronize(w->b_st);  // a batch never waited for
   free_part(w->part);
   free_list(w->allocs);
@@ -1281,7 +1294,11 @@ static void free_workspace(Workspace* w) {
   delete w;
 }
 
+static void aql_drain(Engine& e);  // aql.inc
+static void aql_free(struct AqlState* st);
+
 void device_free(Engine& e) {
+  aql_drain(e);  // (dispatched joins read the snapshot: none may run past here)
   part_comm_free(e);
   if (e.delta_scratch) {
     (void)hipSetDevice(e.device);
@@ -1309,6 +1326,9 @@ void device_free(Engine& e) {
     e.ws_pool.clear();
     e.part_ws = nullptr;
   }
+  aql_free(e.aql);
+  e.aql = nullptr;
+  e.aql_tried = false;
   if (e.free_stream) {  // device_init makes a new one for the next snapshot
     (void)hipSetDevice(e.device);
     (void)hipStreamSynchronize((hipStream_t)e.free_stream);
@@ -1394,6 +1414,7 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 #include "closure.inc"
 #include "bidir.inc"
 #include "labels.inc"
+#include "aql.inc"
 
 // Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
 // (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
@@ -1736,6 +1757,12 @@ void ensure_pool(Engine& e) {
   if (e.part_world > 1) return;  // a partitioned engine runs on its own workspace (part_ws)
   std::lock_guard<std::mutex> lk(e.ws_mu);
   while (e.ws_pool.size() < pool_cap(e)) e.ws_pool.push_back(create_workspace(e));
+  if (!e.aql_tried) {
+    e.aql_tried = true;
+    e.aql = aql_init(e);
+  }
+  if (e.aql)
+    for (Workspace* w : e.ws_pool) (void)aql_workspace(*w);  // (one without: its batches launch through HIP)
 }
 
 // `want` (1 or 2) free workspaces of the pool, taken together: a caller never holds one while it
@@ -2061,6 +2088,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
   if (timing_env) HIP_OK(hipMemsetAsync(w.timing, 0, w.timing_cap * 8, st));
+  const bool ctr_was_clean = w.ctr_clean && !timing_env;
   if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));  // + b_ctrs
   w.ctr_clean = false;
   // GCK_FLAG_PROFILE: one event opens stage A, one closes it, on every 4th batch of the workspace
@@ -2088,8 +2116,23 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // in flight: 9.2 vs 10.3 G checks/s; solo stage A 16.1 vs 12.3 us — every wave waits for its
   // write-through acks before its block arrives), so off by default.
   static const bool coherent_pub = getenv("GCK_COHERENT_PUBLISH") && atoi(getenv("GCK_COHERENT_PUBLISH")) != 0;
-  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub);
-  const uint32_t coherent = w.b_own_stream ? 1u : 0u;
+  // a device batch on the engine's stream whose join runs alone (no events, no chained bundles, no
+  // memset before it on the HIP stream) is dispatched into the engine's HSA queue (aql.inc): its
+  // packet's release fence and completion signal end it, so it publishes itself, without k_publish
+  const bool aql_ok = w.b_own_stream && !host_out && !w.b_timed && !w.b_chained && ctr_was_clean && e.aql &&
+                      w.aql_kernarg && (lj || cj);
+  w.b_aql = false;
+  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub || aql_ok);
+  const uint32_t coherent = (w.b_own_stream && !aql_ok) ? 1u : 0u;
+  // the join into the HSA queue when aql_ok and the code object has this variant
+  auto aql_try = [&](const char* name, const void* args, size_t bytes, uint32_t blocks) {
+    if (!aql_ok) return false;
+    const AqlKernel* k = aql_kernel(e.aql, name);
+    if (!k) return false;
+    aql_dispatch(*e.aql, w, *k, args, bytes, blocks);
+    w.b_aql = true;
+    return true;
+  };
   if (lj) {
     // the label join (labels.inc): one round of slot lines per check; what it leaves goes to the
     // wave bundles through the same deferred list as the closure join's
@@ -2113,7 +2156,13 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.coherent = coherent;
       w.b_seq = j.seq;
     }
-    lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
+    static const char* const lj_names[4] = {"void gck::k_label_join<24, 16u>(gck::LjArgs)",
+                                            "void gck::k_label_join<24, 32u>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 16u>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 32u>(gck::LjArgs)"};
+    const int v = (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
+    if (!aql_try(lj_names[v], &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves)))
+      lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
   } else if (cj) {
     CjArgs j{};
     j.items = d_items;
@@ -2151,7 +2200,15 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     const dim3 grid((n + cpw * kWaves - 1) / (cpw * kWaves)), block(kBlock);
     hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
     const bool small = j.table_bytes <= kCjLdsBytesSmall;
-    if (cpw32 && ds.slot_bits == 24 && small)
+    struct {
+      Ctx c;
+      CjArgs j;
+    } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
+    static_assert(offsetof(decltype(cj_args), j) == 328, "k_closure_join kernarg layout (Ctx, CjArgs)");
+    if (cpw32 && ds.slot_bits == 24 && small &&
+        aql_try("void gck::k_closure_join<24, 2048u, 32u>(gck::Ctx, gck::CjArgs)", &cj_args, sizeof(cj_args),
+                grid.x)) {
+    } else if (cpw32 && ds.slot_bits == 24 && small)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32>), grid, block, 0, st, e0, e1, 0, c, j);
     else if (ds.slot_bits == 24 && small)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
@@ -2177,7 +2234,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
-  if (!self_pub || !w.b_closure) publish_launch(w, st);
+  if (!w.b_aql && (!self_pub || !w.b_closure)) publish_launch(w, st);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
@@ -2187,6 +2244,7 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n);
 // grid-wide path, synchronously. Returns the device time of the batch.
 static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
+  if (w.b_aql) aql_wait(*e.aql, w);  // (the kernel has ended: its publication is complete)
   wait_published(w, st, w.b_seq);
   add_counters(e, w, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
@@ -2205,6 +2263,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     e.stats.closure_checks += n - n_cj;
     e.stats.slot_checks += n - n_cj - tasks;
     if (w.b_label) e.stats.label_checks += n - n_cj;
+    if (w.b_aql) e.stats.aql_batches++;
   }
   // recent batches with leftovers make the next ones chain their bundles on the device
   if (w.b_closure) {

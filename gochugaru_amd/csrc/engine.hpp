@@ -205,6 +205,10 @@ struct Engine {
   // batches to come that chain the wave bundles behind the join in stage A (engine.hip
   // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none
   std::atomic<int> defer_recent{0};
+  // direct AQL dispatch of the join kernels (engine.hip aql.inc): the engine's HSA queue and the
+  // kernels of libgck_kernels.co, set up at the first snapshot (null: launches go through HIP)
+  struct AqlState* aql = nullptr;
+  bool aql_tried = false;
   ~Engine();
 };
 

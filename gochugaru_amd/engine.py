@@ -127,7 +127,7 @@ class _Stats(C.Structure):
                 ("giant_ms", C.c_double), ("deferred_wide", C.c_uint64),
                 ("bidir_checks", C.c_uint64), ("bundles", C.c_uint64), ("closure_checks", C.c_uint64),
                 ("caveat_evals", C.c_uint64), ("caveat_passes", C.c_uint64), ("slot_checks", C.c_uint64),
-                ("label_checks", C.c_uint64)]
+                ("label_checks", C.c_uint64), ("aql_batches", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h

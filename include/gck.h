@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 8
+#define GCK_ABI_VERSION 9
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -222,6 +222,9 @@ typedef struct gck_stats {
                                   alone (one read each) */
   uint64_t label_checks;       /* of closure_checks: those the label join (labels.inc k_label_join,
                                   or its partitioned form) answered */
+  uint64_t aql_batches;        /* batches whose join the engine dispatched into its own HSA queue
+                                  (engine-stream device batches, aql.inc) instead of launching it
+                                  through HIP */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

@@ -44,8 +44,8 @@ def test_struct_layouts_match_header():
     assert E.TUPLE_DTYPE.itemsize == 32
     assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
-    assert C.sizeof(E._Stats) == 224
-    assert E.load_library().gck_abi_version() == 8
+    assert C.sizeof(E._Stats) == 232
+    assert E.load_library().gck_abi_version() == 9
 
 
 @pytest.fixture()

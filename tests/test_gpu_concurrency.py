@@ -3,6 +3,7 @@ workspaces, gck_check_submit / gck_check_wait, checks racing Watch batches, cons
 (consistency.Full after gck_set_head_revision, AtLeast) that the client's retry
 (client/client.go:193-211) carries over, and the permanent error for a Snapshot revision the
 engine has moved past. Every result is compared with the oracle."""
+import os
 import threading
 import time
 
@@ -314,6 +315,9 @@ def test_engine_stream_results_read_right_after_wait(family):
             rolled = (want[-k:] + want[:-k]) if k else want
             assert _got(copies[k][0].cpu().numpy(), copies[k][1].cpu().numpy()) == rolled, (rnd, k)
     torch.cuda.synchronize()
+    if family == "nested" and os.path.exists(os.path.join(os.path.dirname(E.__file__), "libgck_kernels.co")):
+        # the closure join of these batches went into the engine's HSA queue (aql.inc)
+        assert e.stats()["aql_batches"] > 0, e.stats()
     e.close()
 
 
