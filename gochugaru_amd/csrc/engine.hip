@@ -2120,7 +2120,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // memset before it on the HIP stream) is dispatched into the engine's HSA queue (aql.inc): its
   // packet's release fence and completion signal end it, so it publishes itself, without k_publish
   const bool aql_ok = w.b_own_stream && !host_out && !w.b_timed && !w.b_chained && ctr_was_clean && e.aql &&
-                      w.aql_kernarg && (lj || cj);
+                      w.aql_kernarg && !w.cav_on && (lj || cj);
   w.b_aql = false;
   const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub || aql_ok);
   const uint32_t coherent = (w.b_own_stream && !aql_ok) ? 1u : 0u;
@@ -2609,6 +2609,22 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   w.b_cav_req = w.b_cav_err = 0;
   w.fail_code = 0;
   w.fail_msg.clear();
+  // host batches over pinned request buffers (gck_host_alloc) on the AQL path: zero-copy — the
+  // join reads the items from and writes the results into the caller's buffers across PCIe, so a
+  // batch is one packet (no copy-engine transfers, no runtime calls); its later stages, if any,
+  // do the same. GCK_ZERO_COPY=0: the DMA path below.
+  static const bool zc_on = !(getenv("GCK_ZERO_COPY") && atoi(getenv("GCK_ZERO_COPY")) == 0);
+  if (host && zc_on && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) &&
+      host_pinned(e, items, (size_t)n * sizeof(gck_item)) && host_pinned(e, perm, n) &&
+      host_pinned(e, err, (size_t)n * 4)) {
+    host = false;
+    w.b_own_stream = true;
+    w.b_hperm = nullptr;
+    w.b_herr = nullptr;
+    w.b_items = items;
+    w.b_dperm = perm;
+    w.b_derr = err;
+  }
   if (host) {
     // items: a DMA straight from the caller's buffer when it is pinned (gck_host_alloc), else
     // through the workspace's pinned staging (one host copy, one DMA); results likewise
