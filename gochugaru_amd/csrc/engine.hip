@@ -2205,10 +2205,17 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       CjArgs j;
     } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
     static_assert(offsetof(decltype(cj_args), j) == 328, "k_closure_join kernarg layout (Ctx, CjArgs)");
-    if (cpw32 && ds.slot_bits == 24 && small &&
-        aql_try("void gck::k_closure_join<24, 2048u, 32u>(gck::Ctx, gck::CjArgs)", &cj_args, sizeof(cj_args),
+    // half slots (the first 32 B of each slot, closure.inc HALF): GCK_CJ_HALF=0 reads whole lines
+    static const bool half = !(getenv("GCK_CJ_HALF") && atoi(getenv("GCK_CJ_HALF")) == 0);
+    if (cpw32 && ds.slot_bits == 24 && small && half &&
+        aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args, sizeof(cj_args),
                 grid.x)) {
-    } else if (cpw32 && ds.slot_bits == 24 && small)
+    } else if (cpw32 && ds.slot_bits == 24 && small && !half &&
+               aql_try("void gck::k_closure_join<24, 2048u, 32u, false>(gck::Ctx, gck::CjArgs)", &cj_args,
+                       sizeof(cj_args), grid.x)) {
+    } else if (cpw32 && ds.slot_bits == 24 && small && half)
+      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32, true>), grid, block, 0, st, e0, e1, 0, c, j);
+    else if (cpw32 && ds.slot_bits == 24 && small)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32>), grid, block, 0, st, e0, e1, 0, c, j);
     else if (ds.slot_bits == 24 && small)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
