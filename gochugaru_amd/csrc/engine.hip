@@ -35,6 +35,7 @@
 #include <cstring>
 #include <exception>
 #include <fstream>
+#include <functional>
 #include <sstream>
 #include <string>
 #include <thread>
