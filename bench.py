@@ -13,7 +13,7 @@ time). Configs 2, 3, 5 (``--config``) run the same way with their own defaults.
 Also printed: the roofline of the dominant kernel (SURVEY.md §8d algorithmic bytes of a batch,
 counted by the oracle's counting mode, / the mean k_closure_join launch time from the kernel's
 own HIP events, batches one at a time after the timed region; `traffic` = HBM bytes per batch
-from rocprofv3 PMC, tools/gpu.sh profile -> profiles/r03/traffic.json), the PCIe-inclusive rate over
+from rocprofv3 PMC, tools/gpu.sh profile -> profiles/r03/final/traffic.json), the PCIe-inclusive rate over
 host buffers (never `value`), and a CPU baseline: the C restatement oracle (16 host threads) on a
 bounded sample of the same batches, ~15 s of CPU work, with every sampled check compared against
 the GPU's answer (`oracle_agreement`).
@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-max-batches", type=int, default=400)
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "final", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/gpu.sh profile, calibrated by tools/gather_probe)")
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None,
