@@ -150,7 +150,8 @@ struct Workspace {
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
-  void* aql_kernarg = nullptr;  // aql.inc: pinned kernarg block of the dispatched join
+  void* aql_kernarg = nullptr;  // aql.inc: kernarg block of the dispatched join (pinned host memory, or VRAM)
+  bool aql_devargs = false;     // ... in VRAM (GCK_AQL_DEVARGS)
   uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
   void* aql_queue = nullptr;    // aql.inc: the engine queue this workspace dispatches into
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
@@ -1763,7 +1764,7 @@ void ensure_pool(Engine& e) {
     e.aql = aql_init(e);
   }
   if (e.aql)
-    for (Workspace* w : e.ws_pool) (void)aql_workspace(*w);  // (one without: its batches launch through HIP)
+    for (Workspace* w : e.ws_pool) (void)aql_workspace(*e.aql, *w);  // (one without: its batches launch through HIP)
 }
 
 // `want` (1 or 2) free workspaces of the pool, taken together: a caller never holds one while it
