@@ -151,7 +151,7 @@ struct Workspace {
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
   void* aql_kernarg = nullptr;  // aql.inc: kernarg block of the dispatched join (pinned host memory, or VRAM)
-  bool aql_devargs = false;     // ... in VRAM (GCK_AQL_DEVARGS)
+  bool aql_devargs = false;     // ... in VRAM (aql.inc AqlState::devargs)
   uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
   void* aql_queue = nullptr;    // aql.inc: the engine queue this workspace dispatches into
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
