@@ -268,6 +268,23 @@ def launch_ranks(n):
     sys.exit(rc if rc > 0 else (1 if rc else 0))
 
 
+def init_group(backend):
+    """torch.distributed's process group, its first collective run: Gloo announces its connections
+    on stdout when they are made, and stdout is kept for the one JSON line."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group(backend)
+        if backend == "gloo":
+            dist.barrier()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def selftest(args):
     """The multi-rank bookkeeping without a GPU (tests/test_bench_launch.py): every rank joins the
     gloo group, times a dummy step, and rank 0 prints the JSON line's rank-dependent keys."""
@@ -276,7 +293,7 @@ def selftest(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
+        init_group("gloo")
     from gochugaru_amd.sharded import slices
     b, e = slices(args.batch * world, world)[rank]
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
@@ -316,7 +333,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # replicated mode: gloo for the timing barriers / reductions only (no data-path collective);
         # partitioned mode: the per-level exchange (RCCL over xGMI by default)
-        dist.init_process_group(args.part_backend if args.partitioned else "gloo")
+        init_group(args.part_backend if args.partitioned else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

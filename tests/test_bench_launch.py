@@ -26,8 +26,8 @@ def _run(args, env=None, timeout=180):
 def test_launcher_forms_n_ranks(n):
     r = _run(["--gpus", str(n), "--selftest", "--batch", "1000"])
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout  # rank 0 only
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # rank 0's JSON line and nothing else
     out = json.loads(lines[0])
     assert out["n_gpus"] == n
     assert out["max_over_ranks"] == float(n)  # every rank took part in the MAX reduction
