@@ -52,6 +52,43 @@ def test_config4_1e9_full_batch():
     assert 0.3 < np.mean(cp == 2) < 0.7
 
 
+def test_config4_1e9_partitioned_rccl_one_rank():
+    """Config 4 in partitioned mode (BASELINE config 4's "graph partitioned by resource ID") at
+    1e9 tuples through gck_part_check — the partitioned label join with its RCCL exchange, then
+    the level loop for what it leaves — on a one-rank communicator (the test box has one GPU):
+    one 64K batch bit-exact against the C oracle, every check decided by the label join."""
+    from gochugaru_amd.engine import Engine
+    from gochugaru_amd.partition import RcclPartitionedChecker
+    G = synth.build(1e9, device="cuda")
+    items = synth.checks(G, N, seed=4243)
+    e = Engine(device=0, max_batch=N)
+    e.set_partition(0, 1)
+    e.load_schema(synth.SCHEMA)
+    e.reserve_objects(synth.T_USER, G.n_users)
+    e.reserve_objects(synth.T_GROUP, G.n_groups)
+    e.reserve_objects(synth.T_DOC, G.n_docs)
+    e.begin_snapshot(1)
+    keep = []
+    for rel, st, sr, n_rows, off, nbr in G.csrs():
+        off32 = off.to(torch.int32).contiguous()
+        keep.append(off32)
+        e.load_csr(rel, st, sr, n_rows, off32.data_ptr(), nbr.data_ptr(), nbr.numel(), device=True)
+    torch.cuda.synchronize()
+    e.commit_snapshot()
+    pc = RcclPartitionedChecker(e)
+    e.reset_stats()
+    perm, err = pc.check(items, N)
+    gp, ge = perm.cpu().numpy(), err.cpu().numpy()
+    st = e.stats()
+    e.close()
+    _, prog, tab = _oracle(G)
+    hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+    cp, ce, _ = corc.check(prog, tab, hi, threads=THREADS)
+    first, n_bad = _diff(gp, ge, cp, ce)
+    assert n_bad == 0, first
+    assert st["label_checks"] == N, st["label_checks"]
+
+
 @pytest.mark.parametrize("name,scale", [("gdocs", 1.0), ("github", 1.0)], ids=["config2-1e7", "config3-1e8"])
 def test_config2_config3_full_batch(name, scale):
     W = S.CONFIGS[name](scale, device=torch.device("cuda", 0))
