@@ -141,6 +141,8 @@ struct Workspace {
   int32_t* b_derr = nullptr;
   uint8_t* b_hperm = nullptr; // host batch: the caller's result buffers (copied out by the wait)
   int32_t* b_herr = nullptr;
+  uint8_t* b_copy_perm = nullptr;  // zero-copy batch over the pinned staging: the caller's result
+  int32_t* b_copy_err = nullptr;   // buffers the wait copies the staging into
   uint8_t* b_xperm = nullptr; // host batch: where the results' D2H lands — the pinned staging, or
   int32_t* b_xerr = nullptr;  // the caller's buffers themselves when they are gck_host_alloc memory
   bool b_bundles = false;     // stage A is the bundle kernel (else the grid-wide path ran it all)
@@ -2618,21 +2620,32 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   w.b_cav_req = w.b_cav_err = 0;
   w.fail_code = 0;
   w.fail_msg.clear();
-  // host batches over pinned request buffers (gck_host_alloc) on the AQL path: zero-copy — the
-  // join reads the items from and writes the results into the caller's buffers across PCIe, so a
-  // batch is one packet (no copy-engine transfers, no runtime calls); its later stages, if any,
-  // do the same. GCK_ZERO_COPY=0: the DMA path below.
+  // host batches on the AQL path (a snapshot with a one-round join): zero-copy — the join reads
+  // the items from and writes the results into pinned host memory across PCIe (the caller's
+  // gck_host_alloc buffers, or the workspace's staging), so a batch is one packet (no copy-engine
+  // transfers, no runtime calls); its later stages, if any, do the same. GCK_ZERO_COPY=0: the DMA
+  // path below.
   static const bool zc_on = !(getenv("GCK_ZERO_COPY") && atoi(getenv("GCK_ZERO_COPY")) == 0);
+  w.b_copy_perm = nullptr;
+  w.b_copy_err = nullptr;
   if (host && zc_on && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) &&
-      host_pinned(e, items, (size_t)n * sizeof(gck_item)) && host_pinned(e, perm, n) &&
-      host_pinned(e, err, (size_t)n * 4)) {
+      (e.dev->d_cj || e.dev->d_lj)) {
+    const bool pin_in = host_pinned(e, items, (size_t)n * sizeof(gck_item));
+    const bool pin_out = host_pinned(e, perm, n) && host_pinned(e, err, (size_t)n * 4);
+    // pageable buffers go through the workspace's pinned staging — one host copy each way — and
+    // the batch is zero-copy over the staging (no copy engine, no runtime call)
+    if (!pin_in) std::memcpy(w.h_items, items, (size_t)n * sizeof(gck_item));
     host = false;
     w.b_own_stream = true;
     w.b_hperm = nullptr;
     w.b_herr = nullptr;
-    w.b_items = items;
-    w.b_dperm = perm;
-    w.b_derr = err;
+    w.b_items = pin_in ? items : w.h_items;
+    w.b_dperm = pin_out ? perm : w.h_perm;
+    w.b_derr = pin_out ? err : w.h_err;
+    if (!pin_out) {
+      w.b_copy_perm = perm;
+      w.b_copy_err = err;
+    }
   }
   if (host) {
     // items: a DMA straight from the caller's buffer when it is pinned (gck_host_alloc), else
@@ -2723,6 +2736,11 @@ static void finish_batch(Engine& e, Workspace& w) {
 }
 
 static void copy_out(Workspace& w) {
+  if (w.b_copy_perm) {  // a zero-copy batch over the pinned staging: the results to the caller's buffers
+    std::memcpy(w.b_copy_perm, w.h_perm, w.b_n);
+    std::memcpy(w.b_copy_err, w.h_err, (size_t)w.b_n * 4);
+    return;
+  }
   if (!w.b_hperm || w.b_xperm != w.h_perm) return;  // device batch, or results DMA'd in place
   std::memcpy(w.b_hperm, w.h_perm, w.b_n);
   std::memcpy(w.b_herr, w.h_err, (size_t)w.b_n * 4);
