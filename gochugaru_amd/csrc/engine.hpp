@@ -201,6 +201,11 @@ struct Engine {
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
   std::vector<uint64_t> group_scratch;  // group_updates' sort buffers, kept across Watch batches
+  // merged-CSR arrays of retired snapshots kept for the next Watch batch's merge (engine.hip
+  // ralloc / retire_array): bytes -> array, and every array ralloc handed out -> its bytes
+  std::multimap<size_t, void*> recycle;
+  std::unordered_map<void*, size_t> recyclable;
+  size_t recycle_bytes = 0;
   gck_stats stats{};
   // batches to come that chain the wave bundles behind the join in stage A (engine.hip
   // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none
