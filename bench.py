@@ -540,9 +540,10 @@ def main():
         items, (perm, err) = q_rot[args.warm][0], q_out[args.warm]
     st = eng.stats()
     # per-launch time of the dominant kernel, alone on the GPU: the timed batches again, one at a
-    # time, stage A timed by the kernel's own HIP events on its launch stream (every 4th batch of
-    # a workspace). With 3 batches in flight a launch also waits for the CUs the other batches
-    # hold, so the roofline uses these; `achieved_job` is the whole timed region.
+    # time, stage A timed by its dispatch timestamps (the engine's HSA queues; HIP events for a
+    # batch launched through HIP), every 4th batch of a workspace. With batches in flight a launch
+    # also waits for the CUs the other batches hold, so the roofline uses these; `achieved_job` is
+    # the whole timed region.
     st_solo = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and not args.no_profile:
         eng.set_profile(True)  # the timed region ran without events (a timed launch holds back the others)
@@ -686,9 +687,9 @@ def main():
     # ---- roofline of the dominant kernels (SURVEY.md §8d algorithmic bytes) -------------------
     # One batch = stage A (k_closure_join over every check, then k_bundles<1> over what it left) and,
     # rarely, k_bundles<16> (deferred giant checks); they are >99 % of the device time, so stage A
-    # is the "kernel". A timed k_closure_join launch carries its own start / stop events
-    # (hipExtLaunchKernelGGL on the launch stream): they agree with rocprofv3's kernel duration,
-    # where hipEventRecord markers around the launch add ~2.6 us (profiles/r02/evprobe).
+    # is the "kernel". A timed join dispatched into the engine's queue carries the queue's dispatch
+    # timestamps (packet start to completion, the span rocprofv3's kernel trace reports); one
+    # launched through HIP its own start / stop events (hipExtLaunchKernelGGL on the launch stream).
     # Algorithmic bytes come from the oracle's counting mode on the timed batch (implementation
     # independent): 25 B per check (item in, tri-state + error out) + 8 B per row opened + 4 B
     # per edge enumerated (+4 B per caveated edge: none in this config). The launch time is
@@ -724,10 +725,10 @@ def main():
         kname = "k_label_join" if st_roof.get("label_checks", 0) > 0 else "k_closure_join"
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                "kernel": (f"{kname} (+ k_bundles<1> over what it leaves): stage A of a batch, timed by the "
-                           "kernel's own start/stop HIP events (hipExtLaunchKernelGGL) on its launch stream, batches "
-                           "one at a time after the timed region, submitted as in the timed region (engine streams: "
-                           "k_publish follows the join); k_bundles<16> only for deferred giant checks"),
+                "kernel": (f"{kname} (+ k_bundles<1> over what it leaves): stage A of a batch, dispatched as in "
+                           "the timed region (into the engine's HSA queues, aql.inc) and timed by the queue's dispatch "
+                           "timestamps (hsa_amd_profiling_get_dispatch_time: packet start to completion), batches one "
+                           "at a time after the timed region; k_bundles<16> only for deferred giant checks"),
                 "alg_bytes_per_launch": int(b_alg),
                 # the whole job: algorithmic bytes of every timed batch / the timed region (launches
                 # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)

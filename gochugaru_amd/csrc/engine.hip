@@ -2173,8 +2173,12 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // a device batch on the engine's stream whose join runs alone (no events, no chained bundles, no
   // memset before it on the HIP stream) is dispatched into the engine's HSA queue (aql.inc): its
   // packet's release fence and completion signal end it, so it publishes itself, without k_publish
-  const bool aql_ok = w.b_own_stream && !host_out && !w.b_timed && !w.b_chained && ctr_was_clean && e.aql &&
-                      w.aql_kernarg && !w.cav_on && (lj || cj);
+  // (a profiled batch is timed by its queue's dispatch timestamps; under a tracer that intercepts
+  // the queues they are not the packet's own: GCK_AQL_TIMED=0 launches profiled batches through
+  // HIP, timed by their events)
+  static const bool aql_timed = !(getenv("GCK_AQL_TIMED") && atoi(getenv("GCK_AQL_TIMED")) == 0);
+  const bool aql_ok = w.b_own_stream && !host_out && !w.b_chained && ctr_was_clean && e.aql &&
+                      w.aql_kernarg && !w.cav_on && (lj || cj) && (aql_timed || !w.b_timed);
   w.b_aql = false;
   const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub || aql_ok);
   const uint32_t coherent = (w.b_own_stream && !aql_ok) ? 1u : 0u;
@@ -2183,7 +2187,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     if (!aql_ok) return false;
     const AqlKernel* k = aql_kernel(e.aql, name);
     if (!k) return false;
-    aql_dispatch(*e.aql, w, *k, args, bytes, blocks);
+    aql_dispatch(*e.aql, w, *k, args, bytes, blocks, w.b_timed);
     w.b_aql = true;
     return true;
   };
@@ -2311,7 +2315,8 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   w.ctr_clean = true;  // k_publish zeroed the device counters
   const bool profile = w.b_timed;
   float ms = 0.f, bm = 0.f, gm = 0.f;
-  if (w.b_timed) elapsed_ms(&ms, w.ev0, w.ev1);
+  if (w.b_timed && w.b_aql) ms = aql_elapsed_ms(*e.aql, w);  // (its queue's dispatch timestamps)
+  else if (w.b_timed) elapsed_ms(&ms, w.ev0, w.ev1);
   bm = ms;
   const uint32_t n_cj = w.b_closure ? w.h_bctrs[4] : 0u;
   if (n_cj > n) throw Error(GCK_E_DEVICE, "engine invariant violated: closure-join deferred count");

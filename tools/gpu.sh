@@ -49,8 +49,11 @@ case "$CMD" in
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/gwrite" -o gwrite --output-format csv -- $GP > "$OUT/gather_write.jsonl" 2> "$OUT/gather_write.err"
       echo "calibration done"
     fi
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --host-steps 0 "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt1" -o kt1 --output-format csv -- python3 bench.py --no-cpu --host-steps 0 --inflight 1 "$@" > "$OUT/kt1.json" 2> "$OUT/kt1.err"
+    # (under the tracer the queues' dispatch timestamps are not the packets' own: the bench's solo
+    # phase is launched through HIP and timed by its events, GCK_AQL_TIMED=0; the timed region and
+    # the trace are the AQL-dispatched joins)
+    GCK_AQL_TIMED=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --host-steps 0 "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
+    GCK_AQL_TIMED=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt1" -o kt1 --output-format csv -- python3 bench.py --no-cpu --host-steps 0 --inflight 1 "$@" > "$OUT/kt1.json" 2> "$OUT/kt1.err"
     echo "kernel trace done"
     # counter passes launch every kernel through HIP (GCK_AQL=0): the same kernels and bytes, on
     # queues the profiler's counter collection owns (with the engine's own HSA queues it stalls)
