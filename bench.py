@@ -6,9 +6,13 @@ MI355X): tests/synth.py builds the seeded graph on every rank (identical, replic
 engine ingests it through the C ABI (gck_load_csr), and each step is one 65,536-item
 ``doc#view@user`` batch per GPU with the items already resident in HBM: 2,000 distinct
 pre-generated batches, 8 in flight (gck_check_submit / gck_check_wait on the engine's own
-streams, driven by the compiled loop of libgck_driver.so). Ranks check independent batches (no
-collective on the data path), so scaling is weak: value = (checks of all ranks) / (max-over-ranks
-time). Configs 2, 3, 5 (``--config``) run the same way with their own defaults.
+streams, driven by the compiled loop of libgck_driver.so). With N ranks every 64K request is cut
+into N contiguous slices, rank r checking slice r against its replica (no collective on the data
+path): the node figure at batch 64K, strong scaling, value = (checks of the requests) /
+(max-over-ranks time); `weak_scaling` times every rank on its own 64K requests beside it.
+`baseline_step` is BASELINE.md:40-41's own step (one batch alone, H2D + kernels + D2H, median over
+>= 20 batches after 3 warm-up ones). Configs 2, 3 run the same way; 5 (``--config mixed``) checks
+a batch per rank and step.
 
 Also printed: the roofline of the dominant kernel (SURVEY.md §8d algorithmic bytes of a batch,
 counted by the oracle's counting mode, / the mean k_closure_join launch time from the kernel's
@@ -287,7 +291,8 @@ def init_group(backend):
 
 def selftest(args):
     """The multi-rank bookkeeping without a GPU (tests/test_bench_launch.py): every rank joins the
-    gloo group, times a dummy step, and rank 0 prints the JSON line's rank-dependent keys."""
+    gloo group, takes its slice of the request the node figure shares (strong scaling), times a
+    dummy step, and rank 0 prints the JSON line's rank-dependent keys with every rank's slice."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -295,13 +300,19 @@ def selftest(args):
     if world > 1:
         init_group("gloo")
     from gochugaru_amd.sharded import slices
-    b, e = slices(args.batch * world, world)[rank]
+    b, e = slices(args.batch, world)[rank]
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    sl = torch.tensor([b, e], dtype=torch.int64)
+    every = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_gather(every, sl)
+    else:
+        every = [sl]
     if rank == 0:
         print(json.dumps({"n_gpus": world, "max_over_ranks": float(t[0]), "slice": [b, e],
-                          "global_batch": args.batch * world}), flush=True)
+                          "slices": [[int(x[0]), int(x[1])] for x in every], "global_batch": args.batch,
+                          "checks_per_step": {"strong": args.batch, "weak": world * args.batch}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -450,13 +461,21 @@ def main():
             eng.check_bulk_device(it.data_ptr(), args.batch, q_out[k][0].data_ptr(), q_out[k][1].data_ptr(),
                                   stream=stream, contexts=texts)
     else:
-        # distinct batches, rotated through warm-up and timed steps (no step re-reads a batch a
-        # previous step left in the caches), each with its own result buffers; up to `depth`
-        # of them in flight on as many streams (gck_check_submit / gck_check_wait)
+        # distinct requests of args.batch checks, rotated through warm-up and timed steps (no step
+        # re-reads a batch a previous step left in the caches), each with its own result buffers;
+        # up to `depth` of them in flight on as many streams (gck_check_submit / gck_check_wait).
+        # The node figure (BASELINE "whole node at batch 64K"): every request is the
+        # same on every rank and each rank checks its contiguous slice of it (sharded.slices, as
+        # DistributedChecker does), so N GPUs share one 64K request — strong scaling; at N = 1
+        # the slice is the whole request. Weak scaling (every rank its own 64K requests) is
+        # timed after it as a secondary key.
+        from gochugaru_amd.sharded import slices
+        s_lo, s_hi = slices(args.batch, world)[rank]
+        n_slice = s_hi - s_lo
         n_rot = args.warm + args.steps
-        rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(n_rot)]
-        outs = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
-                 torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
+        rot = [WL.checks(args.batch, 1000 + k)[s_lo:s_hi].contiguous() for k in range(n_rot)]
+        outs = [(torch.zeros(n_slice, dtype=torch.uint8, device=dev),
+                 torch.zeros(n_slice, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
         streams = [torch.cuda.Stream(dev) for _ in range(depth)]
         torch.cuda.synchronize()
         cursor = {"k": 0}
@@ -467,7 +486,7 @@ def main():
             cursor["k"] += 1
             if len(pending) >= depth:
                 pending.popleft().wait()
-            pending.append(eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
+            pending.append(eng.submit(rot[k].data_ptr(), n_slice, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
                                       device=True, stream=streams[k % depth].cuda_stream,
                                       engine_stream=bool(args.engine_streams)))
 
@@ -487,7 +506,7 @@ def main():
                 ks = range(k0, k0 + count)
                 prepared[len(prepared)] = (count, eng.prepare_batches(
                     [rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
-                    [outs[k][1].data_ptr() for k in ks], args.batch, depth,
+                    [outs[k][1].data_ptr() for k in ks], n_slice, depth,
                     [streams[(k - k0) % depth].cuda_stream for k in ks], engine_streams=bool(args.engine_streams)))
 
             def run_steps(count):
@@ -534,6 +553,38 @@ def main():
         _driver().gckd_set_trace(None, 0)
     progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms"
              + (f" (compiled loop {loop_s['s'] * 1e3:.3f} ms)" if native else ""))
+    # weak scaling beside the node figure (N > 1): every rank checks its own whole requests
+    weak = None
+    if native and world > 1 and WL.kind in ("nested", "gdocs", "github") and not args.partitioned:
+        n_w = min(args.steps, 500)
+        n_wr = n_w + 2 * depth
+        w_rot = [WL.checks(args.batch, 700000 + 100003 * rank + k) for k in range(n_wr)]
+        w_out = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
+                  torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(n_wr)]
+        mkw = lambda ks: eng.prepare_batches([w_rot[k].data_ptr() for k in ks], [w_out[k][0].data_ptr() for k in ks],
+                                             [w_out[k][1].data_ptr() for k in ks], args.batch, depth,
+                                             [streams[j % depth].cuda_stream for j in range(len(ks))],
+                                             engine_streams=bool(args.engine_streams))
+        w_warm, w_run = mkw(range(2 * depth)), mkw(range(2 * depth, n_wr))
+        torch.cuda.synchronize()
+        w_warm.run()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        tw = time.perf_counter()
+        w_run.run()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tw = time.perf_counter() - tw
+        tt = torch.tensor([tw], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tw = float(tt[0])
+        weak = {"value": round(world * args.batch * n_w / tw, 1), "unit": "checks/s", "steps": n_w,
+                "ms_per_step": round(tw / n_w * 1e3, 4), "scaling": "weak",
+                "note": f"every rank checks its own {args.batch}-check requests ({world} x {args.batch} checks per "
+                        f"step), max-over-ranks time"}
+        del w_rot, w_out
+        progress("weak-scaling phase done")
     if WL.kind not in ("mixed", "quota") and not args.partitioned:  # the first timed batch and its results
         items, (perm, err) = rot[args.warm], outs[args.warm]
     if WL.kind == "quota":
@@ -549,7 +600,7 @@ def main():
         eng.set_profile(True)  # the timed region ran without events (a timed launch holds back the others)
         eng.reset_stats()
         for k in range(min(len(rot), 48)):
-            eng.submit(rot[k].data_ptr(), args.batch, outs[k][0].data_ptr(), outs[k][1].data_ptr(), device=True,
+            eng.submit(rot[k].data_ptr(), n_slice, outs[k][0].data_ptr(), outs[k][1].data_ptr(), device=True,
                        stream=streams[0].cuda_stream, engine_stream=bool(args.engine_streams)).wait()
         torch.cuda.synchronize()
         st_solo = eng.stats()
@@ -560,7 +611,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt[0])
 
-    total_checks = world * args.batch * args.steps
+    # pipelined configs: N ranks share each request (strong scaling); the others check a batch per
+    # rank and step (weak)
+    strong = WL.kind in ("nested", "gdocs", "github") and not args.partitioned
+    total_checks = (args.batch if strong else world * args.batch) * args.steps
     value = total_checks / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     if args.partitioned:  # this rank's slice of the global batch, for the checker below
@@ -575,6 +629,7 @@ def main():
     # the same rotated batches, `depth` in flight (gck_check_submit with host buffers: each
     # batch's copies overlap the other batches' kernels), and one at a time for reference.
     host_rate = None
+    baseline_step = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and args.host_steps > 0:
         # (up to 32 of the rotated batches, cycled: pinned host memory per batch is 1.6 MB)
         n_h = min(len(rot), max(32, args.warm + 1))
@@ -605,7 +660,7 @@ def main():
             t0 = time.perf_counter()
             r = host_run(args.host_steps, dq, pinned)
             dt = time.perf_counter() - t0
-            return r, {"value": round(args.host_steps * args.batch / dt, 1),
+            return r, {"value": round(args.host_steps * n_slice / dt, 1),
                        "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
 
         def timed_native(dq):
@@ -613,17 +668,39 @@ def main():
             ks = [j % len(p_rot) for j in range(args.host_steps)]
             wk = [j % len(p_rot) for j in range(args.warm)]
             mk = lambda kk: eng.prepare_batches([p_rot[k][0].ctypes.data for k in kk], [p_rot[k][1].ctypes.data for k in kk],
-                                                [p_rot[k][2].ctypes.data for k in kk], args.batch, dq, host=True)
+                                                [p_rot[k][2].ctypes.data for k in kk], n_slice, dq, host=True)
             warm_run, run = mk(wk), mk(ks)
             warm_run.run()
             dt = run.run()
             k0_ = ks[-1]
             return {k0_: (p_rot[k0_][1].copy(), p_rot[k0_][2].copy())}, {
-                "value": round(args.host_steps * args.batch / dt, 1), "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
+                "value": round(args.host_steps * n_slice / dt, 1), "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
         nres, main = timed_native(depth)
         hres, py_pinned = timed(depth, True)
         pres, pageable = timed(depth, False)
         _, one = timed(1, True)
+        # BASELINE.md:40-41's own definition: 3 warm-up batches, then >= 20 batches, each one alone
+        # (items H2D, kernels, results D2H on the batch's stream: the compiled loop over pinned
+        # buffers, 1 in flight), checks/s = checks per batch / the MEDIAN batch time
+        from gochugaru_amd.engine import _driver
+        import ctypes
+        nb_med = max(20, min(200, args.host_steps))
+        kb = [j % len(p_rot) for j in range(3 + nb_med)]
+        med_run = eng.prepare_batches([p_rot[k][0].ctypes.data for k in kb], [p_rot[k][1].ctypes.data for k in kb],
+                                      [p_rot[k][2].ctypes.data for k in kb], n_slice, 1, host=True)
+        stamps = np.zeros(2 * len(kb), dtype=np.float64)
+        _driver().gckd_set_trace(stamps.ctypes.data_as(ctypes.c_void_p), len(kb))
+        med_run.run()
+        _driver().gckd_set_trace(None, 0)
+        ends = stamps[1::2]
+        per_batch = (ends - np.concatenate([[0.0], ends[:-1]]))[3:]
+        med_s = float(np.median(per_batch))
+        baseline_step = {"value": round(n_slice / med_s, 1), "unit": "checks/s", "median_batch_ms": round(med_s * 1e3, 4),
+                         "p90_batch_ms": round(float(np.percentile(per_batch, 90)) * 1e3, 4),
+                         "batches": int(len(per_batch)), "warmup_batches": 3, "checks_per_batch": n_slice,
+                         "definition": "BASELINE.md:40-41: checks per batch / median batch time over >= 20 batches "
+                                       "after 3 warm-up batches, each batch alone (1 in flight): items H2D + kernels + "
+                                       "results D2H (pinned gck_host_alloc buffers, the compiled submit/wait loop)"}
         k0 = args.warm % len(h_rot)
         kn = (args.host_steps - 1) % len(p_rot)
         refn = (outs[kn][0].cpu().numpy(), outs[kn][1].cpu().numpy())
@@ -710,7 +787,7 @@ def main():
                 ck = corc.check(prog, tab, hk, threads=threads)[2]
             cnt.update(ck)
         cnt = {k: v / n_cnt for k, v in cnt.items()}
-        b_alg = 25 * args.batch + 8 * cnt["rows"] + 4 * cnt["edges"]
+        b_alg = 25 * len(hk) + 8 * cnt["rows"] + 4 * cnt["edges"]
         ms_a = st_roof["bundle_ms"] / st_roof["bundle_launches"]
         ms_b = st_roof["giant_ms"] / st_roof["bundle_launches"]
         ms = ms_a + ms_b
@@ -800,6 +877,8 @@ def main():
                          f"compared with the GPU result"}
 
     progress("oracle / CPU baseline done")
+    import shutil
+    spicedb = shutil.which("spicedb")  # SpiceDB serve-testing is the baseline where present
     if rank == 0 and WL.kind in ("mixed", "quota") and not args.no_oracle:
         agree = agree_mixed
     if rank == 0 and WL.kind in ("quota", "mixed") and not args.no_oracle and not args.no_cpu and world == 1:
@@ -827,18 +906,31 @@ def main():
                        f"permission checks/sec (whole node) at batch 64K, {WL.cfg['workload']}"),
             "value": round(value, 1), "unit": "checks/s", "n_gpus": 1 if args.share_gpu else world, "steps": args.steps,
             "warmup": args.warmup, "warmup_batches": args.warm, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32",
             "data": WL.data,
             "config": {**WL.cfg, "tuples": n_tuples, "batch_per_gpu": args.batch,
                        "parallelism": (f"graph partitioned x{world} by resource id, per-level all-to-all "
                                        f"({args.part_backend}), global batch {args.batch * world}")
                        if args.partitioned else
-                       (f"batch-sharded x{world}: one process per GPU, each rank checks its own stream of "
+                       (f"batch-sharded x{world}: one process per GPU, each {args.batch}-check request cut into "
+                        f"{world} contiguous slices (sharded.slices), rank r checks slice r against a full replica of "
+                        f"the graph; no data-path collective (barriers and the max-over-ranks time only)"
+                        if strong else
+                        f"batch-sharded x{world}: one process per GPU, each rank checks its own stream of "
                         f"{args.batch}-check batches against a full replica of the graph; no data-path collective "
                         f"(barriers and the max-over-ranks time only)"
                         + (f", {world} ranks sharing one GPU" if args.share_gpu else "")),
                        "hbm_snapshot_GB": round(dev_bytes / 1e9, 2)},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof,
+            "cpu_baseline": ({**cpu, "spicedb_probe": {"which_spicedb": spicedb,
+                                                       "note": "BASELINE.md: SpiceDB serve-testing (memdb) is the CPU "
+                                                               "baseline where a spicedb binary exists on the box; "
+                                                               + ("it does, but it is not driven by this bench"
+                                                                  if spicedb else
+                                                                  "none was found, so the C restatement stands in")}}
+                             if cpu else cpu),
+            **({"baseline_step": baseline_step} if baseline_step else {}),
+            **({"weak_scaling": weak} if weak else {}),
             **({"host_buffers": host_rate} if host_rate else {}),
             "oracle_agreement": agree,
             **({"disagreements": disagree} if disagree else {}),

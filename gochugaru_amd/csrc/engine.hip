@@ -1659,9 +1659,8 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     // snapshot change holds the engine exclusively): return them to the pool on the engine's
     // own non-blocking stream, where a free costs a fraction of one on the legacy null stream,
     // which must order itself after every blocking stream
-    static const bool null_free = getenv("GCK_FREE_NULL") != nullptr;  // A/B
     const size_t n_free = e.dev->allocs.size();
-    if (e.free_stream && !null_free) {
+    if (e.free_stream) {
       for (void* p : e.dev->allocs) retire_array(e, p, (hipStream_t)e.free_stream);
       e.dev->allocs.clear();
     } else {
@@ -2165,11 +2164,9 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // the join publishes the batch itself unless something must follow it first: a host batch's
   // copies, the chained bundles, or — for a device batch on the engine's stream, whose caller has
   // no stream to order its reads after the kernel's end — the end-of-kernel L2 write-back
-  // (k_publish after the join). GCK_COHERENT_PUBLISH=1 publishes those from the join too, with
-  // the results written through the L2 (store_result, `coherent`): measured slower (config 4, 8
-  // in flight: 9.2 vs 10.3 G checks/s; solo stage A 16.1 vs 12.3 us — every wave waits for its
-  // write-through acks before its block arrives), so off by default.
-  static const bool coherent_pub = getenv("GCK_COHERENT_PUBLISH") && atoi(getenv("GCK_COHERENT_PUBLISH")) != 0;
+  // (k_publish after the join). (Publishing those from the join too, with the results written
+  // through the L2, was measured slower — config 4, 8 in flight: 9.2 vs 10.3 G checks/s; every
+  // wave waits for its write-through acknowledgements before its block arrives — and removed.)
   // a device batch on the engine's stream whose join runs alone (no events, no chained bundles, no
   // memset before it on the HIP stream) is dispatched into the engine's HSA queue (aql.inc): its
   // packet's release fence and completion signal end it, so it publishes itself, without k_publish
@@ -2180,8 +2177,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   const bool aql_ok = w.b_own_stream && !host_out && !w.b_chained && ctr_was_clean && e.aql &&
                       w.aql_kernarg && !w.cav_on && (lj || cj) && (aql_timed || !w.b_timed);
   w.b_aql = false;
-  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || coherent_pub || aql_ok);
-  const uint32_t coherent = (w.b_own_stream && !aql_ok) ? 1u : 0u;
+  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok);
+  const uint32_t coherent = 0u;  // (results are published by the kernel end's write-back)
   // the join into the HSA queue when aql_ok and the code object has this variant
   auto aql_try = [&](const char* name, const void* args, size_t bytes, uint32_t blocks) {
     if (!aql_ok) return false;
@@ -2250,33 +2247,24 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     }
     // a timed batch's events are the kernel's own start and stop (hipExtLaunchKernel), not markers
     // around its dispatch, so they agree with a profiler's kernel duration
-    // 32 checks per wave: each wave waits for the slowest of 64 lines instead of 128 (solo launch
-    // 12.1-12.3 vs 12.8-12.9 us, the same throughput, profiles/r02/sweep/cpw*); GCK_CJ_CPW=64 for
-    // the other
-    static const bool cpw32 = !(getenv("GCK_CJ_CPW") && atoi(getenv("GCK_CJ_CPW")) == 64);
-    const uint32_t cpw = cpw32 ? 32u : 64u;
+    // 32 checks per wave where the slot entries are 24-bit and the table is small: each wave waits
+    // for the slowest of 64 lines instead of 128 (solo launch 12.1-12.3 vs 12.8-12.9 us, the same
+    // throughput, profiles/r02/sweep/cpw*)
+    const bool small = j.table_bytes <= kCjLdsBytesSmall;
+    const bool fast = ds.slot_bits == 24 && small;
+    const uint32_t cpw = fast ? 32u : 64u;
     const dim3 grid((n + cpw * kWaves - 1) / (cpw * kWaves)), block(kBlock);
     hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
-    const bool small = j.table_bytes <= kCjLdsBytesSmall;
     struct {
       Ctx c;
       CjArgs j;
     } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
     static_assert(offsetof(decltype(cj_args), j) == 328, "k_closure_join kernarg layout (Ctx, CjArgs)");
-    // half slots (the first 32 B of each slot, closure.inc HALF): GCK_CJ_HALF=0 reads whole lines
-    static const bool half = !(getenv("GCK_CJ_HALF") && atoi(getenv("GCK_CJ_HALF")) == 0);
-    if (cpw32 && ds.slot_bits == 24 && small && half &&
-        aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args, sizeof(cj_args),
-                grid.x)) {
-    } else if (cpw32 && ds.slot_bits == 24 && small && !half &&
-               aql_try("void gck::k_closure_join<24, 2048u, 32u, false>(gck::Ctx, gck::CjArgs)", &cj_args,
-                       sizeof(cj_args), grid.x)) {
-    } else if (cpw32 && ds.slot_bits == 24 && small && half)
+    // (half slots: the first 32 B of each resource slot, closure.inc HALF)
+    if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
+                        sizeof(cj_args), grid.x)) {
+    } else if (fast)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32, true>), grid, block, 0, st, e0, e1, 0, c, j);
-    else if (cpw32 && ds.slot_bits == 24 && small)
-      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32>), grid, block, 0, st, e0, e1, 0, c, j);
-    else if (ds.slot_bits == 24 && small)
-      hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall>), grid, block, 0, st, e0, e1, 0, c, j);
     else if (ds.slot_bits == 24)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytes>), grid, block, 0, st, e0, e1, 0, c, j);
     else if (small)
@@ -2678,12 +2666,11 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   // host batches on the AQL path (a snapshot with a one-round join): zero-copy — the join reads
   // the items from and writes the results into pinned host memory across PCIe (the caller's
   // gck_host_alloc buffers, or the workspace's staging), so a batch is one packet (no copy-engine
-  // transfers, no runtime calls); its later stages, if any, do the same. GCK_ZERO_COPY=0: the DMA
-  // path below.
-  static const bool zc_on = !(getenv("GCK_ZERO_COPY") && atoi(getenv("GCK_ZERO_COPY")) == 0);
+  // transfers, no runtime calls); its later stages, if any, do the same. Without the AQL path
+  // (GCK_AQL=0, a profiled batch): the DMA path below.
   w.b_copy_perm = nullptr;
   w.b_copy_err = nullptr;
-  if (host && zc_on && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) &&
+  if (host && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) &&
       (e.dev->d_cj || e.dev->d_lj)) {
     const bool pin_in = host_pinned(e, items, (size_t)n * sizeof(gck_item));
     const bool pin_out = host_pinned(e, perm, n) && host_pinned(e, err, (size_t)n * 4);

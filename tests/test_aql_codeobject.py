@@ -20,7 +20,6 @@ KERNELS = {
     "void gck::k_label_join<24, 32u>(gck::LjArgs)": [112],
     "void gck::k_label_join<32, 16u>(gck::LjArgs)": [112],
     "void gck::k_label_join<32, 32u>(gck::LjArgs)": [112],
-    "void gck::k_closure_join<24, 2048u, 32u, false>(gck::Ctx, gck::CjArgs)": [328, 128],
     "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [328, 128],
 }
 
@@ -68,4 +67,12 @@ def test_dispatched_kernels_present_with_their_kernarg_layout():
         assert kinds.get("hidden_group_size_x") == hid + 12, (dm, kinds)
         if "hidden_grid_dims" in kinds:
             assert kinds["hidden_grid_dims"] == hid + 64, (dm, kinds)
-        assert hid + 72 <= seg <= 1024, (dm, seg)  # aql.inc kAqlKernargBytes
+        assert seg == hid + 256 and seg <= 1024, (dm, seg)  # the whole hidden block; aql.inc kAqlKernargBytes
+
+
+def test_code_object_carries_the_build_id():
+    """aql.inc kBuildId: the code object exports the variable aql_init compares with the library's."""
+    if not os.path.exists(CO) or not os.path.exists(READELF):
+        pytest.skip("code object or llvm-readelf missing")
+    syms = subprocess.run([READELF, "--syms", CO], capture_output=True, text=True, check=True).stdout
+    assert "gck_kernels_build_id" in syms

@@ -31,7 +31,15 @@ def test_launcher_forms_n_ranks(n):
     out = json.loads(lines[0])
     assert out["n_gpus"] == n
     assert out["max_over_ranks"] == float(n)  # every rank took part in the MAX reduction
-    assert out["global_batch"] == 1000 * n and out["slice"] == [0, 1000]
+    # the node figure: one 1000-check request shared by the n ranks in contiguous slices, in rank
+    # order, covering it exactly (strong scaling); weak scaling checks n x 1000 per step
+    assert out["global_batch"] == 1000
+    sl = out["slices"]
+    assert len(sl) == n and sl[0][0] == 0 and sl[-1][1] == 1000
+    assert all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+    assert max(e - b for b, e in sl) - min(e - b for b, e in sl) <= 1
+    assert out["slice"] == sl[0]
+    assert out["checks_per_step"] == {"strong": 1000, "weak": 1000 * n}
 
 
 def test_launcher_refuses_missing_gpus():

@@ -10,6 +10,7 @@
 #                                                        calibration, and traffic.json
 #   bash tools/gpu.sh phases <tag> [bench args]          bench with GCK_DEBUG_PHASES=1 (snapshot / Watch
 #                                                        phase times on stderr)
+#   bash tools/gpu.sh pmcprobe <tag> [bench args]        one FETCH_SIZE pass over the AQL path (GCK_DEBUG_AQL)
 set -e
 CMD=$1
 TAG=$2
@@ -68,6 +69,19 @@ case "$CMD" in
     find "$OUT" -name "*kernel_trace.csv" -delete
     find "$OUT" -name "*counter_collection.csv" -delete
     find "$OUT" -name "*agent_info.csv" -delete
+    ;;
+  pmcprobe)
+    # a counter pass over the AQL path itself (the engine's own HSA queues), with the dispatch / wait
+    # diagnostics of GCK_DEBUG_AQL on stderr; killed after 120 s if it stalls (run it last)
+    SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --no-cpu --host-steps 0 --inflight 1 $*"
+    GCK_DEBUG_AQL=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/aqlfetch" -o aqlfetch --output-format csv -- $SHORT > "$OUT/aqlfetch.json" 2> "$OUT/aqlfetch.err"
+    rc=$?
+    echo "pmc pass on the AQL path: status $rc"
+    grep "gck aql" "$OUT/aqlfetch.err" | head -30 || true
+    tail -5 "$OUT/aqlfetch.err"
+    find "$OUT" -name "*kernel_trace.csv" -delete
+    find "$OUT" -name "*agent_info.csv" -delete
+    exit $rc
     ;;
   *)
     echo "usage: tools/gpu.sh tests|bench|sweep|profile|phases <tag> [args]" >&2
