@@ -105,7 +105,6 @@ struct DeviceSnapshot {
   std::vector<unsigned char> lj_host;
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
-  bool part_full = false;     // partitioned engine, first snapshot: every row present until part_finish_upload
   std::vector<uint64_t> lj_key;  // what the label tables were built from (labels.inc: reused while unchanged)
   std::vector<void*> lj_ptrs;    // their arrays (in allocs or hallocs)
   uint64_t lj_bytes = 0;
@@ -290,6 +289,10 @@ struct Ctx {
   Entry* outbox;
   unsigned* out_cnt;
   uint32_t out_cap;
+  // query / join ids this launch may allocate below (spawn_join): query_cap / join_cap, or on a
+  // partitioned graph the end of this rank's own id range (partition.inc part_loop)
+  uint32_t q_hi, j_hi;
+  uint32_t force_exact;  // every root runs exact-depth (partitioned graphs: no global heights)
 };
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -441,6 +444,7 @@ __device__ __forceinline__ int64_t csr_exp(const DevCSR& r, uint32_t p) { return
 // Is the check of permission node p on object obj an exact-depth check (its root can reach the
 // depth budget)? obj must be a known object of the node's type.
 __device__ __forceinline__ bool deep_root(const Ctx& c, const DevNode* nodes, uint32_t p, uint32_t obj) {
+  if (c.force_exact) return true;
   if (!(nodes[p].flags & NF_DEEP) || !c.hgt) return false;
   const unsigned long long h = gptr(c.hgt)[p];
   return h != 0 && gptr(reinterpret_cast<const uint32_t*>(h))[obj] >= c.max_depth;
@@ -675,11 +679,11 @@ __device__ __forceinline__ void spawn_join(const Ctx& c, uint32_t q, uint32_t ob
   }
   unsigned j = atomicAdd(&c.ctr->n_joins, 1u);
   unsigned q0 = atomicAdd(&c.ctr->n_queries, n_ops);
-  if (j >= c.join_cap) {
+  if (j >= c.j_hi) {
     atomicOr(&c.ctr->overflow, 16u);
     return;
   }
-  if (q0 + n_ops > c.query_cap) {
+  if (q0 + n_ops > c.q_hi) {
     atomicOr(&c.ctr->overflow, 8u);
     return;
   }
@@ -743,11 +747,11 @@ __device__ __forceinline__ void spawn_and(const Ctx& c, uint32_t q, uint32_t obj
   if (vinsert(c, make_key(c, q, node, tag, depth, obj)) <= 0) return;
   unsigned j = atomicAdd(&c.ctr->n_joins, 1u);
   unsigned q0 = atomicAdd(&c.ctr->n_queries, 1u);
-  if (j >= c.join_cap) {
+  if (j >= c.j_hi) {
     atomicOr(&c.ctr->overflow, 16u);
     return;
   }
-  if (q0 + 1 > c.query_cap) {
+  if (q0 + 1 > c.q_hi) {
     atomicOr(&c.ctr->overflow, 8u);
     return;
   }
@@ -1045,6 +1049,21 @@ __device__ __forceinline__ void finalize(const Ctx& c, uint32_t qi, uint32_t res
   }
 }
 
+__device__ __forceinline__ void resolve_query(const Ctx& c, uint32_t qi) {
+  DevQuery* q = &c.queries[qi];
+  uint32_t f = qflags(q);
+  if (f & QF_DONE) return;
+  if (f & QF_FOUND_Y) {
+    finalize(c, qi, GCK_PERM_HAS);
+    return;
+  }
+  if (q->last_alive > c.level) return;  // entries pushed for the next level
+  int pend = __hip_atomic_load(&q->pending_joins, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  if (pend != 0) return;
+  f = qflags(q);
+  finalize(c, qi, result_from_flags(f));
+}
+
 __global__ void __launch_bounds__(kBlock) k_resolve(Ctx c) {
   // after an overflow some allocated queries/joins were never written: the batch is re-run
   // split in half, so do not touch them
@@ -1052,20 +1071,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(Ctx c) {
   const uint32_t nq = min(__hip_atomic_load(&c.ctr->n_queries, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                           c.query_cap);
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x; qi < nq; qi += stride) {
-    DevQuery* q = &c.queries[qi];
-    uint32_t f = qflags(q);
-    if (f & QF_DONE) continue;
-    if (f & QF_FOUND_Y) {
-      finalize(c, qi, GCK_PERM_HAS);
-      continue;
-    }
-    if (q->last_alive > c.level) continue;  // entries pushed for the next level
-    int pend = __hip_atomic_load(&q->pending_joins, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (pend != 0) continue;
-    f = qflags(q);
-    finalize(c, qi, result_from_flags(f));
-  }
+  for (uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x; qi < nq; qi += stride) resolve_query(c, qi);
 }
 
 // Publish this level's counts and reset the per-level counters (one lane, after k_resolve).
@@ -1317,10 +1323,7 @@ static void free_list(std::vector<void*>& list) {
 }
 
 static void free_part(PartState* p);  // partition.inc
-static void partition_filter(const Engine& e, DeviceSnapshot& ds, DevCSR& d, uint64_t& ne);
-struct CsrInfo;
-static void part_finish_upload(Engine& e, DeviceSnapshot& ds, std::vector<DevNode>& nodes, std::vector<DevCSR>& table,
-                               std::vector<CsrInfo>& info, const std::vector<size_t>& later);
+static void part_filter_device(const Engine& e, DeviceSnapshot& ds, const HostCSR& h, DevCSR& d, uint64_t& ne);
 
 static void aql_workspace_free(Workspace& w);  // aql.inc
 
@@ -1483,11 +1486,8 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
   try {
     std::vector<DevCSR> table;
     std::vector<CsrInfo> info;
-    // a partitioned engine's first snapshot: the heights and the label tables (labels.inc: the
-    // replicated hierarchy labels, the slots of this rank's subjects and resources) are built from
-    // every row as loaded, then each CSR keeps the rows this rank owns
-    std::vector<size_t> part_later;
-    ds->part_full = e.part_world > 1 && !delta;
+    // (a partitioned engine's CSRs hold what this rank keeps — engine.hpp part_keep — already
+    // filtered at ingest; a device CSR the caller loaded is filtered while it is copied)
     for (HostCSR& h : csrs) {
       DevCSR d{};
       d.n_rows = h.n_rows;
@@ -1519,6 +1519,18 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
         ds->base.push_back(b);
         continue;
       }
+      if (h.dev_off && e.part_world > 1) {  // partitioned graph: only the edges this rank keeps (partition.inc)
+        part_filter_device(e, *ds, h, d, ne);
+        b.n_edges = ne;
+        if (ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+          build_mhash(*ds, d, ne);
+          b.mh_keys = ne;
+        }
+        table.push_back(d);
+        info.push_back({ne, h.stype});
+        ds->base.push_back(b);
+        continue;
+      }
       uint32_t* off = dalloc<uint32_t>(ds->allocs, (size_t)h.n_rows + 1, &ds->bytes);
       uint32_t* nbr = dalloc<uint32_t>(ds->allocs, ne, &ds->bytes);
       if (h.dev_off) {
@@ -1539,16 +1551,6 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
         }
         d.cav = cav;
         d.exp_us = ex;
-      }
-      if (e.part_world > 1 && delta) {  // partitioned graph: keep the rows this rank owns (partition.inc)
-        partition_filter(e, *ds, d, ne);
-        b.n_edges = ne;
-      } else if (e.part_world > 1) {  // ... after the label tables are built from every row (below)
-        part_later.push_back(table.size());
-        table.push_back(d);
-        info.push_back({ne, h.stype});
-        ds->base.push_back(b);
-        continue;
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
@@ -1582,7 +1584,6 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     pc.mark("bidir");
     build_labels(e, *ds, nodes, items, table, info);
     pc.mark("labels");
-    if (ds->part_full) part_finish_upload(e, *ds, nodes, table, info, part_later);
     for (size_t k = 0; k < ds->base.size(); ++k)  // indexes built for local probes (bidir.inc)
       if (table[k].mhash && !ds->base[k].mh_keys) ds->base[k].mh_keys = ds->base[k].n_edges;
     ds->table = table;
@@ -1882,11 +1883,16 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.ctr = w.ctr;
   c.frontier_cap = (uint32_t)w.frontier_cap;
   c.seg_cap = (uint32_t)std::min<size_t>(w.seg_cap, (1u << 24) - 1);
-  const uint32_t q_bits = ds.any_deep ? ds.q_bits_deep : ds.q_bits;
+  // a partitioned graph (world > 1) runs every check exact-depth (partition.inc): the deep layout
+  const bool deep = ds.any_deep || e.part_world > 1;
+  const uint32_t q_bits = deep ? ds.q_bits_deep : ds.q_bits;
   c.query_cap = (uint32_t)std::min<size_t>(w.query_cap, 1ull << q_bits);
   c.join_cap = (uint32_t)w.join_cap;
+  c.q_hi = c.query_cap;
+  c.j_hi = c.join_cap;
+  c.force_exact = 0;
   c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
-  if (ds.any_deep) {  // exact-depth checks key their entries by depth (make_key)
+  if (deep) {  // exact-depth checks key their entries by depth (make_key)
     const uint32_t db = ceil_log2((uint64_t)c.max_depth + 1);
     c.depth_shift = 34;
     c.depth_mask = (1u << db) - 1u;
@@ -2259,7 +2265,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       Ctx c;
       CjArgs j;
     } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
-    static_assert(offsetof(decltype(cj_args), j) == 328, "k_closure_join kernarg layout (Ctx, CjArgs)");
+    static_assert(offsetof(decltype(cj_args), j) == 336, "k_closure_join kernarg layout (Ctx, CjArgs)");
     // (half slots: the first 32 B of each resource slot, closure.inc HALF)
     if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
                         sizeof(cj_args), grid.x)) {
@@ -2926,14 +2932,6 @@ static Workspace& part_workspace(Engine& e) {
 static PartState& part_state(Workspace& w) {
   if (!w.part) w.part = new PartState();
   return *w.part;
-}
-
-static void free_part(PartState* p) {
-  if (!p) return;
-  free_xfer(p->xfer);
-  free_join(p->pj);
-  if (p->h_out) (void)hipHostFree(p->h_out);
-  delete p;  // outbox / out_cnt are in the workspace's allocation list
 }
 
 #include "delta.inc"

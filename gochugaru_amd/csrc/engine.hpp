@@ -158,6 +158,9 @@ struct Engine {
   int device = 0;
   uint32_t part_rank = 0, part_world = 1;  // partitioned graph (gck_set_partition)
   bool part_set = false;                   // gck_set_partition was called (any world, one rank too)
+  // the schema's hub nodes and the relations of their hierarchy (labels.inc partition_rules): what
+  // a rank keeps beyond the rows it owns (part_keep)
+  std::vector<char> part_hub_node, part_hub_rel;
   bool device_ready = false;
   std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
   std::unique_ptr<Schema> schema;
@@ -189,8 +192,7 @@ struct Engine {
   std::condition_variable ws_cv;
   std::vector<Workspace*> ws_pool;
   Workspace* part_ws = nullptr;   // the partitioned batch's own workspace (partition.inc)
-  uint64_t part_generation = 0;   // the snapshot generation a partitioned batch started on
-  void* part_comm = nullptr;      // ncclComm_t of gck_part_init (partition.inc)
+  void* part_comm = nullptr;      // the RCCL communicator of gck_part_init (partition.inc RcclCtx)
   std::mutex stats_mu;            // stats are added by concurrent batches
   std::mutex host_mu;             // pinned host buffers handed out by gck_host_alloc (base -> bytes)
   std::map<uintptr_t, size_t> host_bufs;
@@ -227,6 +229,18 @@ struct PhaseClock {
   void mark(const char* phase);
   ~PhaseClock();
 };
+
+// Partitioned graphs: does rank e.part_rank keep the tuple rel(obj) <- (sid, srel)?
+// Its own rows (part_owner(obj)); and of a hub relation (partition_rules) every userset and
+// wildcard tuple — the replicated hierarchy — and the tuples of the subjects it owns (their user
+// slots). Every ingest path applies it (staging, gck_load_csr, Watch batches) after interning, so
+// that ids and caveat instances stay the same on every rank.
+inline bool part_keep(const Engine& e, uint16_t rel, uint32_t obj, uint32_t sid, uint16_t srel) {
+  if (e.part_world <= 1 || part_owner(obj, e.part_world) == e.part_rank) return true;
+  if (rel >= e.part_hub_rel.size() || !e.part_hub_rel[rel]) return false;
+  return srel != kEllipsis || sid == kWildcard || part_owner(sid, e.part_world) == e.part_rank;
+}
+void partition_rules(Engine& e);  // labels.inc: e.part_hub_node / part_hub_rel from the schema
 
 // snapshot.cpp
 void add_tuples_text(Engine& e, const char* text, size_t len);
@@ -291,26 +305,15 @@ void device_lookup(Engine& e, Workspace& w, const gck_item& proto, bool vary_res
                    int64_t now_us, std::vector<uint32_t>& ids, std::vector<uint8_t>& perms);
 void device_lookup_subjects(Engine& e, Workspace& w, const gck_item& proto, int64_t now_us, std::vector<uint32_t>& ids,
                             std::vector<uint8_t>& perms);
-// partitioned checks (partition.inc), one BFS level per expand / ingest / resolve round
-void part_begin(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
-void part_expand(Engine& e, uint64_t* send_counts);
-// sync = false: the caller orders the next work on the partitioned batch's stream itself
-// (gck_part_check: RCCL on the same stream), so the step does not wait for its copies / kernels
-void part_pack(Engine& e, void* d_send, size_t send_cap, bool sync = true);
-void part_ingest(Engine& e, const void* d_recv, size_t n_recv, void* d_flags, bool sync = true);
-uint32_t part_resolve(Engine& e, const void* d_flags);
-void part_finish(Engine& e, uint8_t* d_perm, int32_t* d_err);
+// partitioned checks (partition.inc): one batch over every rank, the exchange over RCCL inside
+// libgck (part_check, after part_init) or the caller's transport (part_check_with)
 void part_unique_id(uint8_t* out);
 void part_init(Engine& e, const uint8_t* id);
 void part_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, uint8_t* d_perm, int32_t* d_err,
                 void* stream);
+void part_check_with(Engine& e, const gck_transport& t, const gck_item* d_items, size_t n, int64_t now_us,
+                     uint8_t* d_perm, int32_t* d_err, void* stream);
 void part_comm_free(Engine& e);
-// the partitioned label join (partition.inc): records (check, user slot) for the owners of the
-// resources, and their decision there
-void part_join_pack(Engine& e, const gck_item* d_items, size_t n, void* d_send, size_t send_cap, uint64_t* counts,
-                    void* stream);
-void part_join_decide(Engine& e, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv, uint8_t* d_perm,
-                      int32_t* d_err, void* stream);
 void device_free(Engine& e);
 
 }  // namespace gck

@@ -197,6 +197,7 @@ int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
     std::unique_lock<std::shared_mutex> lk(e.mu);
     drain_batches(e);
     e.schema = std::move(sc);
+    partition_rules(e);
     e.schema_text.assign(text ? text : "", len);
     e.interner.assign(e.schema->types.size(), TypeInterner());
     reset_caveats(e);
@@ -399,14 +400,24 @@ int gck_load_csr(gck_engine* ge, uint16_t relation, uint16_t subject_type, uint1
     h.ext = false;
     h.n_rows = n_rows;
     h.n_edges = n_edges;
-    if (mem_flags & GCK_MEM_DEVICE) {
+    if (mem_flags & GCK_MEM_DEVICE) {  // (a partitioned engine copies only what it keeps: device_upload)
       h.dev_off = offsets;
       h.dev_nbr = neighbours;
     } else {
       REQUIRE(offsets[n_rows] == n_edges && offsets[0] == 0, GCK_E_INVALID_ARGUMENT,
               "gck_load_csr: offsets do not span the neighbour array");
-      h.off.assign(offsets, offsets + (size_t)n_rows + 1);
-      h.nbr.assign(neighbours, neighbours + n_edges);
+      if (e.part_world > 1) {  // partitioned graph: the rows and subjects this rank keeps (part_keep)
+        h.off.assign((size_t)n_rows + 1, 0);
+        for (uint32_t r = 0; r < n_rows; ++r) {
+          for (uint32_t k = offsets[r]; k < offsets[r + 1]; ++k)
+            if (part_keep(e, relation, r, neighbours[k], subject_relation)) h.nbr.push_back(neighbours[k]);
+          h.off[r + 1] = (uint32_t)h.nbr.size();
+        }
+        h.n_edges = h.nbr.size();
+      } else {
+        h.off.assign(offsets, offsets + (size_t)n_rows + 1);
+        h.nbr.assign(neighbours, neighbours + n_edges);
+      }
     }
     e.prebuilt.push_back(std::move(h));
   });
@@ -493,9 +504,11 @@ static void apply_updates(Engine& e, uint64_t revision, const gck_update* ups, s
               std::to_string(e.revision));
   PhaseClock pc("watch");
   std::vector<gck_update> mine;
-  if (e.part_world > 1) {  // partitioned graph: this rank keeps the rows it owns
-    for (size_t i = 0; i < n; ++i)
-      if (part_owner(ups[i].tuple.resource_id, e.part_world) == e.part_rank) mine.push_back(ups[i]);
+  if (e.part_world > 1) {  // partitioned graph: the updates of what this rank keeps (part_keep)
+    for (size_t i = 0; i < n; ++i) {
+      const gck_tuple& t = ups[i].tuple;
+      if (part_keep(e, t.relation, t.resource_id, t.subject_id, t.subject_relation)) mine.push_back(ups[i]);
+    }
     ups = mine.data();
     n = mine.size();
   }
@@ -787,94 +800,18 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
     Engine& e = need(ge);
     REQUIRE(world >= 1 && world <= 63 && rank < world, GCK_E_INVALID_ARGUMENT, "bad rank / world");
     std::unique_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(!e.committed && !e.dev && e.ws_pool.empty() && !e.part_ws, GCK_E_STATE,
-            "gck_set_partition must precede the first snapshot");
+    REQUIRE(!e.committed && !e.dev && e.ws_pool.empty() && !e.part_ws && e.staged.empty() && e.prebuilt.empty(),
+            GCK_E_STATE, "gck_set_partition must precede the first snapshot");
     e.part_rank = rank;
     e.part_world = world;
     e.part_set = true;
+    partition_rules(e);
     if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR;  // both need the whole graph
   });
 }
 
 uint32_t gck_partition_owner(uint32_t object_id, uint32_t world) {
   return world <= 1 ? 0u : part_owner(object_id, world);
-}
-
-int gck_part_begin(gck_engine* ge, const gck_item* d_items, size_t n, int64_t now_us, void* stream) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
-    REQUIRE(n == 0 || d_items, GCK_E_INVALID_ARGUMENT, "null items");
-    part_begin(e, d_items, n, now_us, stream);
-  });
-}
-
-int gck_part_expand(gck_engine* ge, uint64_t* send_counts) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(send_counts, GCK_E_INVALID_ARGUMENT, "null counts");
-    part_expand(e, send_counts);
-  });
-}
-
-int gck_part_pack(gck_engine* ge, void* d_send, size_t send_cap) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(d_send || !send_cap, GCK_E_INVALID_ARGUMENT, "null buffer");
-    part_pack(e, d_send, send_cap);
-  });
-}
-
-int gck_part_ingest(gck_engine* ge, const void* d_recv, size_t n_recv, void* d_flags) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(d_flags && (d_recv || !n_recv), GCK_E_INVALID_ARGUMENT, "null buffers");
-    part_ingest(e, d_recv, n_recv, d_flags);
-  });
-}
-
-int gck_part_resolve(gck_engine* ge, const void* d_flags, uint32_t* out_active) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(d_flags && out_active, GCK_E_INVALID_ARGUMENT, "null argument");
-    *out_active = part_resolve(e, d_flags);
-  });
-}
-
-int gck_part_finish(gck_engine* ge, uint8_t* d_out_perm, int32_t* d_out_err) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    part_finish(e, d_out_perm, d_out_err);
-  });
-}
-
-int gck_part_join_pack(gck_engine* ge, const gck_item* d_items, size_t n, void* d_send, size_t send_cap,
-                       uint64_t* send_counts, void* stream) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
-    REQUIRE(send_counts && (n == 0 || d_items) && (d_send || !send_cap), GCK_E_INVALID_ARGUMENT, "null argument");
-    part_join_pack(e, d_items, n, d_send, send_cap, send_counts, stream);
-  });
-}
-
-int gck_part_join_decide(gck_engine* ge, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv,
-                         uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
-  return guard([&] {
-    Engine& e = need(ge);
-    std::shared_lock<std::shared_mutex> lk(e.mu);
-    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
-    REQUIRE((n == 0 || (d_items && d_out_perm && d_out_err)) && (d_recv || !n_recv), GCK_E_INVALID_ARGUMENT,
-            "null argument");
-    part_join_decide(e, d_items, n, d_recv, n_recv, d_out_perm, d_out_err, stream);
-  });
 }
 
 int gck_part_unique_id(uint8_t* out) {
@@ -901,6 +838,18 @@ int gck_part_check(gck_engine* ge, const gck_item* d_items, size_t n, int64_t no
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
     part_check(e, d_items, n, now_us, d_out_perm, d_out_err, stream);
+  });
+}
+
+int gck_part_check_with(gck_engine* ge, const gck_transport* t, const gck_item* d_items, size_t n, int64_t now_us,
+                        uint8_t* d_out_perm, int32_t* d_out_err, void* stream) {
+  return guard([&] {
+    Engine& e = need(ge);
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
+    REQUIRE(t, GCK_E_INVALID_ARGUMENT, "null transport");
+    REQUIRE(n == 0 || (d_items && d_out_perm && d_out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
+    part_check_with(e, *t, d_items, n, now_us, d_out_perm, d_out_err, stream);
   });
 }
 

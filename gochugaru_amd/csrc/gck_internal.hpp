@@ -19,12 +19,16 @@
 namespace gck {
 
 // Partitioned graphs (partition.inc): the rank that owns object `obj` (its CSR
-// rows, its frontier entries). Type-independent, so an object id means the same owner in every
-// relation; a multiplicative hash spreads consecutive ids.
-GCK_HD inline uint32_t part_owner(uint32_t obj, uint32_t world) {
-  uint32_t h = obj * 2654435761u;
-  h ^= h >> 16;
-  return h % world;
+// rows, its slots, its frontier entries), and the object's index among that rank's objects.
+// Type-independent, so an object id means the same owner in every relation. Ids are interned in
+// arrival order, so id mod world is already a hash of the external id that spreads every type
+// evenly; and the owner's objects are then ids rank, rank + world, ... — a rank's slot tables
+// hold exactly its own objects, indexed by obj / world, with no translation table.
+GCK_HD inline uint32_t part_owner(uint32_t obj, uint32_t world) { return obj % world; }
+GCK_HD inline uint32_t part_local(uint32_t obj, uint32_t world) { return obj / world; }
+// Objects [0, count) of a type that rank `rank` of `world` owns.
+GCK_HD inline uint32_t part_local_count(uint32_t count, uint32_t rank, uint32_t world) {
+  return count > rank ? (count - 1 - rank) / world + 1 : 0u;
 }
 
 constexpr uint16_t kEllipsis = 0xFFFFu;

@@ -139,6 +139,7 @@ void validate_tuple(const Engine& e, const gck_tuple& t) {
 
 void stage_tuple(Engine& e, const gck_tuple& t) {
   validate_tuple(e, t);
+  if (!part_keep(e, t.relation, t.resource_id, t.subject_id, t.subject_relation)) return;  // another rank's
   StagedTuple s{};
   s.rel = t.relation;
   s.stype = t.subject_type;
@@ -196,6 +197,10 @@ void stage_tuples(Engine& e, const gck_tuple* t, size_t n) {
       throw Error(code[c], err[c]);
     }
   e.seq += n;
+  if (e.part_world > 1)  // a partitioned graph: what this rank keeps (part_keep), the page validated whole
+    e.staged.erase(std::remove_if(e.staged.begin() + base, e.staged.end(),
+                                  [&](const StagedTuple& s) { return !part_keep(e, s.rel, s.obj, s.sid, s.srel); }),
+                   e.staged.end());
 }
 
 namespace {

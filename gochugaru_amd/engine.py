@@ -132,6 +132,16 @@ class _Stats(C.Structure):
 
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
 _P = C.c_void_p
+
+# gck_transport (include/gck.h): a caller's exchange between the ranks of a partitioned engine
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, _P, _P, C.POINTER(C.c_uint64), _P, C.POINTER(C.c_uint64), _P)
+ALLREDUCE_MAX_U8_FN = C.CFUNCTYPE(C.c_int, _P, _P, C.c_uint64, _P)
+
+
+class Transport(C.Structure):
+    _fields_ = [("ctx", _P), ("alltoallv", ALLTOALLV_FN), ("allreduce_max_u8", ALLREDUCE_MAX_U8_FN)]
+
+
 _SIGS = {
     "gck_abi_version": (C.c_int, []),
     "gck_last_error": (C.c_char_p, []),
@@ -188,14 +198,7 @@ _SIGS = {
                                       C.POINTER(C.c_size_t)]),
     "gck_set_partition": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "gck_partition_owner": (C.c_uint32, [C.c_uint32, C.c_uint32]),
-    "gck_part_begin": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P]),
-    "gck_part_expand": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
-    "gck_part_pack": (C.c_int, [_P, _P, C.c_size_t]),
-    "gck_part_ingest": (C.c_int, [_P, _P, C.c_size_t, _P]),
-    "gck_part_resolve": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
-    "gck_part_finish": (C.c_int, [_P, _P, _P]),
-    "gck_part_join_pack": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t, C.POINTER(C.c_uint64), _P]),
-    "gck_part_join_decide": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t, _P, _P, _P]),
+    "gck_part_check_with": (C.c_int, [_P, C.POINTER(Transport), _P, C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_part_unique_id": (C.c_int, [_P]),
     "gck_part_init": (C.c_int, [_P, _P]),
     "gck_part_check": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
@@ -630,41 +633,6 @@ class Engine:
         _check(self._lib.gck_set_partition(self._h, rank, world))
         self.part_rank, self.part_world = rank, world
 
-    def part_begin(self, d_items: int, n: int, now_us: int = 0, stream: Optional[int] = None):
-        _check(self._lib.gck_part_begin(self._h, d_items, n, now_us, stream))
-
-    def part_expand(self) -> np.ndarray:
-        counts = np.zeros(self.part_world, dtype=np.uint64)
-        _check(self._lib.gck_part_expand(self._h, counts.ctypes.data_as(C.POINTER(C.c_uint64))))
-        return counts
-
-    def part_pack(self, d_send: int, cap_entries: int):
-        _check(self._lib.gck_part_pack(self._h, d_send, cap_entries))
-
-    def part_ingest(self, d_recv: int, n_recv: int, d_flags: int):
-        _check(self._lib.gck_part_ingest(self._h, d_recv, n_recv, d_flags))
-
-    def part_resolve(self, d_flags: int) -> int:
-        out = C.c_uint32()
-        _check(self._lib.gck_part_resolve(self._h, d_flags, C.byref(out)))
-        return out.value
-
-    def part_finish(self, d_perm: int, d_err: int):
-        _check(self._lib.gck_part_finish(self._h, d_perm, d_err))
-
-    def part_join_pack(self, d_items: int, n: int, d_send: int, cap_records: int, stream: Optional[int] = None) -> np.ndarray:
-        """gck_part_join_pack: (check, subject slot) records for the owners of the resources,
-        grouped by rank; returns the record count per destination rank."""
-        counts = np.zeros(self.part_world, dtype=np.uint64)
-        _check(self._lib.gck_part_join_pack(self._h, d_items, n, d_send, cap_records,
-                                            counts.ctypes.data_as(C.POINTER(C.c_uint64)), stream))
-        return counts
-
-    def part_join_decide(self, d_items: int, n: int, d_recv: int, n_recv: int, d_perm: int, d_err: int,
-                         stream: Optional[int] = None):
-        """gck_part_join_decide: the received records' checks, decided into perm / err."""
-        _check(self._lib.gck_part_join_decide(self._h, d_items, n, d_recv, n_recv, d_perm, d_err, stream))
-
     @staticmethod
     def part_unique_id() -> bytes:
         """gck_part_unique_id: the RCCL communicator id rank 0 hands to every rank."""
@@ -682,6 +650,12 @@ class Engine:
                    stream: Optional[int] = None):
         """gck_part_check: the whole partitioned check, exchanged over RCCL inside libgck."""
         _check(self._lib.gck_part_check(self._h, d_items, n, now_us, d_perm, d_err, stream))
+
+    def part_check_with(self, transport: "Transport", d_items: int, n: int, d_perm: int, d_err: int, now_us: int = 0,
+                        stream: Optional[int] = None):
+        """gck_part_check_with: the partitioned check over the caller's transport (a
+        gochugaru_amd.partition transport: gck_transport's callbacks)."""
+        _check(self._lib.gck_part_check_with(self._h, C.byref(transport), d_items, n, now_us, d_perm, d_err, stream))
 
     def stats(self) -> Stats:
         s = _Stats()
@@ -822,14 +796,7 @@ def _context_arrays(contexts):
     return contexts.arr, contexts.lens, len(contexts)
 
 
-PART_ENTRY_BYTES = 12  # GCK_PART_ENTRY_BYTES
-PART_JOIN_RECORD_BYTES = 80  # GCK_PART_JOIN_RECORD_BYTES
 PART_UNIQUE_ID_BYTES = 128  # GCK_PART_UNIQUE_ID_BYTES
-
-
-def part_flag_bytes(n: int) -> int:
-    """GCK_PART_FLAG_BYTES(n)."""
-    return 4 * n + 1
 
 
 def partition_owner(object_id: int, world: int) -> int:

@@ -1,158 +1,160 @@
-"""Host driver of partitioned checks: one BFS level per round, exchanged over torch.distributed.
+"""Partitioned checks across ranks: the exchange of a partitioned engine.
 
-SURVEY.md §8e (BASELINE.json config 4, partitioned mode): graphs above one GPU's 288 GB are
-split by resource id — rank r keeps the CSR rows of the objects it owns
-(``gck_partition_owner``) — and every rank checks the same global batch together. The engine
-(``gck_part_*``, include/gck.h; partition.inc) does the device work of a level; this module moves
-data between ranks:
+SURVEY.md §8e (BASELINE.json config 4, partitioned mode): a graph above one GPU's 288 GB is split
+by object id — rank r keeps the rows of the objects it owns (``gck_partition_owner``: id mod
+world), the replicated hub hierarchy and the hub memberships of the subjects it owns
+(include/gck.h; partition.inc) — and every rank checks the same batch with the others. The engine
+runs the whole batch (the label join, then the exact-depth level loop with joins) inside
+``gck_part_check_with``; it only needs two collectives from its caller (``gck_transport``):
 
-* the entries a rank produced for objects it does not own: counts, then the 12-byte entries,
-  ``all_to_all_single`` — RCCL over xGMI with the ``nccl`` backend (one process per GPU), or
-  host-staged with ``gloo`` (CPU rehearsals, several ranks sharing one GPU);
-* the per-check flag planes (found / conditional / depth error / alive, 4n+1 bytes):
-  ``all_reduce(MAX)``, after which every rank resolves every check identically, so the loop
-  ends on every rank in the same round without another collective.
+* ``alltoallv``: per peer a block of bytes, blocks back to back in rank order on both sides;
+* ``allreduce_max_u8``: an element-wise MAX over the ranks of a byte array, in place.
+
+:class:`GlooTransport` implements them with torch.distributed collectives over host-staged copies
+(gloo: CPU rehearsals, several ranks sharing one GPU); :class:`RcclPartitionedChecker` uses the
+RCCL transport inside libgck (``gck_part_check``; one process per GPU, xGMI).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+import ctypes
+import traceback
+from typing import Optional
 
-import numpy as np
+from .engine import ALLREDUCE_MAX_U8_FN, ALLTOALLV_FN, Engine, Transport
 
-from .engine import PART_ENTRY_BYTES, PART_JOIN_RECORD_BYTES, Engine, part_flag_bytes
+_HIP = None
 
-_WORDS = PART_ENTRY_BYTES // 4  # an entry is three 32-bit words on the wire
-_RWORDS = PART_JOIN_RECORD_BYTES // 4  # a label-join record (check index, 3 reserved, subject slot): 20 words
+
+def _hip():
+    """The HIP runtime this process already uses (the one libgck and torch resolved to)."""
+    global _HIP
+    if _HIP is None:
+        path = "libamdhip64.so"
+        try:
+            for line in open("/proc/self/maps"):
+                if "libamdhip64" in line:
+                    path = line.split()[-1]
+                    break
+        except OSError:
+            pass
+        h = ctypes.CDLL(path)
+        h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        h.hipMemcpy.restype = ctypes.c_int
+        h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        h.hipStreamSynchronize.restype = ctypes.c_int
+        _HIP = h
+    return _HIP
+
+
+class GlooTransport:
+    """gck_transport over torch.distributed collectives on host tensors (any backend that takes
+    CPU tensors: gloo). ``device=True``: the engine's buffers are device memory (copied through
+    the HIP runtime after the engine's stream is synchronised); ``device=False``: host memory
+    (a transport test without a GPU). The first failure is kept in ``error``."""
+
+    def __init__(self, group=None, device: bool = True):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device
+        self.error: Optional[str] = None
+        self.calls = {"alltoallv": 0, "allreduce_max_u8": 0, "bytes": 0}
+        # (the callbacks must outlive every call that may use them)
+        self._a2a = ALLTOALLV_FN(self._alltoallv)
+        self._ar = ALLREDUCE_MAX_U8_FN(self._allreduce)
+        self.c = Transport(None, self._a2a, self._ar)
+
+    def _sync(self, stream):
+        if self.device:
+            rc = _hip().hipStreamSynchronize(stream)
+            if rc != 0:
+                raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+
+    def _copy(self, dst: int, src: int, n: int):
+        if n == 0:
+            return
+        if self.device:
+            rc = _hip().hipMemcpy(dst, src, n, 4)  # hipMemcpyDefault: host or device on either side
+            if rc != 0:
+                raise RuntimeError(f"hipMemcpy failed ({rc})")
+        else:
+            ctypes.memmove(dst, src, n)
+
+    def _alltoallv(self, ctx, send, send_bytes, recv, recv_bytes, stream) -> int:
+        try:
+            torch = self.torch
+            sb = [int(send_bytes[i]) for i in range(self.world)]
+            rb = [int(recv_bytes[i]) for i in range(self.world)]
+            self._sync(stream)
+            hs = torch.empty(sum(sb), dtype=torch.uint8)
+            hr = torch.empty(sum(rb), dtype=torch.uint8)
+            self._copy(hs.data_ptr(), send, sum(sb))
+            self.dist.all_to_all_single(hr, hs, output_split_sizes=rb, input_split_sizes=sb, group=self.group)
+            self._copy(recv, hr.data_ptr(), sum(rb))
+            self.calls["alltoallv"] += 1
+            self.calls["bytes"] += sum(sb)
+            return 0
+        except Exception:  # (an exception may not cross the C ABI)
+            self.error = self.error or traceback.format_exc()
+            return -1
+
+    def _allreduce(self, ctx, buf, n, stream) -> int:
+        try:
+            torch = self.torch
+            self._sync(stream)
+            h = torch.empty(int(n), dtype=torch.uint8)
+            self._copy(h.data_ptr(), buf, int(n))
+            self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
+            self._copy(buf, h.data_ptr(), int(n))
+            self.calls["allreduce_max_u8"] += 1
+            return 0
+        except Exception:
+            self.error = self.error or traceback.format_exc()
+            return -1
 
 
 class PartitionedChecker:
-    """Checks global batches on a partitioned engine (``Engine.set_partition`` before the
-    snapshot). Every rank of ``group`` calls :meth:`check` with the same items."""
+    """Checks batches on a partitioned engine (``Engine.set_partition`` before the snapshot) over
+    a torch.distributed group: every rank of ``group`` calls :meth:`check` with the same items and
+    gets every result (``gck_part_check_with`` with a :class:`GlooTransport`)."""
 
     def __init__(self, engine: Engine, group=None):
         import torch
         import torch.distributed as dist
 
         self.engine = engine
-        self.group = group
-        self.dist = dist
         self.torch = torch
         self.world = dist.get_world_size(group)
         assert engine.part_world == self.world and engine.part_rank == dist.get_rank(group), \
             "engine partition (set_partition) must match the process group"
-        self.staged = dist.get_backend(group) != "nccl"  # gloo: exchange through host memory
-        # the engine's device (a CPU model of the protocol sets torch_device, tests/part_model.py)
-        self.device = getattr(engine, "torch_device", None) or torch.device("cuda", torch.cuda.current_device())
-        self.cuda = self.device.type == "cuda"
-        self._send = torch.empty(0, dtype=torch.int32, device=self.device)
-        self.levels = 0
+        self.transport = GlooTransport(group, device=True)
 
-    def _sync(self):
-        if self.cuda:
-            self.torch.cuda.synchronize(self.device)
-
-    def _coll_tensor(self, t):
-        return t.cpu() if self.staged else t
-
-    def _back(self, t_coll, t_dev):
-        if self.staged:
-            t_dev.copy_(t_coll)
-
-    def check(self, d_items, n: int, now_us: int = 0) -> Tuple["torch.Tensor", "torch.Tensor"]:
+    def check(self, d_items, n: int, now_us: int = 0, out=None):
         """``d_items``: a device tensor holding n gck_item records (20 bytes each). Returns
-        (permissionship uint8[n], item error int32[n]) on the device, identical on every rank.
-        First the label join (one all-to-all of (check, subject slot) records to the owners of
-        the resources, an all-reduce MAX of the decided result bytes), then the level loop over
-        what no rank decided, in batch order."""
-        torch, dist = self.torch, self.dist
-        eng = self.engine
-        stream = torch.cuda.current_stream(self.device).cuda_stream if self.cuda else None
-        perm = torch.zeros(n, dtype=torch.uint8, device=self.device)
-        err = torch.zeros(n, dtype=torch.int32, device=self.device)
-        send = torch.empty(max(n, 1) * _RWORDS, dtype=torch.int32, device=self.device)
-        self._sync()
-        counts = eng.part_join_pack(d_items.data_ptr(), n, send.data_ptr(), max(n, 1), stream)
-        send_cnt = torch.from_numpy(counts.astype(np.int64))
-        recv_cnt = torch.zeros(self.world, dtype=torch.int64)
-        if not self.staged:
-            send_cnt, recv_cnt = send_cnt.to(self.device), recv_cnt.to(self.device)
-        dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)
-        rc = recv_cnt.cpu().numpy()
-        n_recv = int(rc.sum())
-        recv = torch.empty(max(n_recv, 1) * _RWORDS, dtype=torch.int32, device=self.device)
-        s_send = self._coll_tensor(send[: int(counts.sum()) * _RWORDS])
-        s_recv = self._coll_tensor(recv[: n_recv * _RWORDS])
-        dist.all_to_all_single(s_recv, s_send, output_split_sizes=[int(c) * _RWORDS for c in rc],
-                               input_split_sizes=[int(c) * _RWORDS for c in counts], group=self.group)
-        self._back(s_recv, recv[: n_recv * _RWORDS])
-        self._sync()
-        eng.part_join_decide(d_items.data_ptr(), n, recv.data_ptr(), n_recv, perm.data_ptr(), err.data_ptr(), stream)
-        f = self._coll_tensor(perm)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-        self._back(f, perm)
-        self._sync()
-        self.joined = int((perm != 0).sum())
-        left = torch.nonzero(perm == 0).flatten()
-        if left.numel() == 0:
-            self.levels = 0
-            return perm, err
-        items2 = d_items.reshape(n, 20)[left].contiguous()
-        p2, e2 = self._loop(items2, int(left.numel()), now_us)
-        perm[left] = p2
-        err[left] = e2
-        return perm, err
-
-    def _loop(self, d_items, n: int, now_us: int = 0):
-        """The level-synchronous loop (gck_part_begin .. gck_part_finish) over d_items."""
-        torch, dist = self.torch, self.dist
-        eng = self.engine
-        stream = torch.cuda.current_stream(self.device).cuda_stream if self.cuda else None
-        flags = torch.zeros(part_flag_bytes(n), dtype=torch.uint8, device=self.device)
-        perm = torch.zeros(n, dtype=torch.uint8, device=self.device)
-        err = torch.zeros(n, dtype=torch.int32, device=self.device)
-        self._sync()
-        eng.part_begin(d_items.data_ptr(), n, now_us, stream)
-        self.levels = 0
-        while True:
-            counts = eng.part_expand()
-            total = int(counts.sum())
-            if self._send.numel() < total * _WORDS:
-                self._send = torch.empty(max(total * _WORDS, 2 * self._send.numel()), dtype=torch.int32,
-                                         device=self.device)
-            if total:
-                eng.part_pack(self._send.data_ptr(), total)
-            send_cnt = torch.from_numpy(counts.astype(np.int64))
-            recv_cnt = torch.zeros(self.world, dtype=torch.int64)
-            if not self.staged:
-                send_cnt, recv_cnt = send_cnt.to(self.device), recv_cnt.to(self.device)
-            dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)
-            rc = recv_cnt.cpu().numpy()
-            n_recv = int(rc.sum())
-            recv = torch.empty(max(n_recv, 1) * _WORDS, dtype=torch.int32, device=self.device)
-            s_send = self._coll_tensor(self._send[: total * _WORDS])
-            s_recv = self._coll_tensor(recv[: n_recv * _WORDS])
-            dist.all_to_all_single(s_recv, s_send, output_split_sizes=[int(c) * _WORDS for c in rc],
-                                   input_split_sizes=[int(c) * _WORDS for c in counts], group=self.group)
-            self._back(s_recv, recv[: n_recv * _WORDS])
-            self._sync()
-            eng.part_ingest(recv.data_ptr(), n_recv, flags.data_ptr())
-            f = self._coll_tensor(flags)
-            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            self._back(f, flags)
-            self._sync()
-            active = eng.part_resolve(flags.data_ptr())
-            self.levels += 1
-            if active == 0:
-                break
-        eng.part_finish(perm.data_ptr(), err.data_ptr())
+        (permissionship uint8[n], item error int32[n]) on the device, identical on every rank."""
+        torch = self.torch
+        if out is None:
+            out = (torch.zeros(n, dtype=torch.uint8, device=d_items.device),
+                   torch.zeros(n, dtype=torch.int32, device=d_items.device))
+        perm, err = out
+        stream = torch.cuda.current_stream(d_items.device).cuda_stream
+        try:
+            self.engine.part_check_with(self.transport.c, d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(),
+                                        now_us, stream)
+        except Exception as ex:
+            if self.transport.error:
+                raise RuntimeError(f"{ex}\ntransport failure:\n{self.transport.error}") from ex
+            raise
         return perm, err
 
 
 class RcclPartitionedChecker:
-    """Checks global batches on a partitioned engine with the level loop and its exchange inside
-    libgck (``gck_part_check``: grouped RCCL send / receive + all-reduce over xGMI, one process
-    per GPU). ``group`` (any torch.distributed backend) only carries the communicator id from
-    rank 0 to the others, once."""
+    """Checks batches on a partitioned engine with the exchange inside libgck (``gck_part_check``:
+    grouped RCCL send / receive and all-reduce over xGMI, one process per GPU). ``group`` (any
+    torch.distributed backend) only carries the communicator id from rank 0 to the others, once."""
 
     def __init__(self, engine: Engine, group=None):
         import torch
@@ -168,18 +170,16 @@ class RcclPartitionedChecker:
         if world > 1:
             dist.broadcast_object_list(box, src=0, group=group)
         engine.part_init(box[0])
-        self._stream = None
 
     def check(self, d_items, n: int, now_us: int = 0, out=None):
         """`out`: (perm uint8[n], err int32[n]) device tensors to write into (a caller's
-        preallocated result buffers); new ones otherwise."""
+        preallocated result buffers); new ones otherwise. Ordered on the caller's current stream
+        (taken at every call)."""
         torch = self.torch
         if out is None:
             out = (torch.zeros(n, dtype=torch.uint8, device=d_items.device),
                    torch.zeros(n, dtype=torch.int32, device=d_items.device))
         perm, err = out
-        if self._stream is None:
-            self._stream = torch.cuda.current_stream(d_items.device).cuda_stream
-        self.engine.part_check(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us, self._stream)
+        stream = torch.cuda.current_stream(d_items.device).cuda_stream
+        self.engine.part_check(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us, stream)
         return perm, err
-

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 9
+#define GCK_ABI_VERSION 10
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -386,62 +386,51 @@ int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resou
                         uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);
 
 /* ---- partitioned graphs (graphs above one GPU's 288 GB) ----------------
- * Rank r of `world` keeps the rows of the objects it owns (gck_partition_owner) and checks a
- * global batch together with the other ranks, one BFS level per round:
- *
- *   gck_part_begin(items)                           every rank, the same device items
- *   loop:
- *     gck_part_expand(counts[world])                expands the level; entries owed to each rank
- *     gck_part_pack(send, cap)                      those entries, grouped by rank (cap: entries)
- *     (caller) all-to-all of counts, then of the entries (GCK_PART_ENTRY_BYTES each)
- *     gck_part_ingest(recv, n_recv, flags)          flags: GCK_PART_FLAG_BYTES(n) device bytes
- *     (caller) all-reduce MAX of the flag bytes, in place
- *     gck_part_resolve(flags, &active)              identical `active` on every rank; 0 = done
- *   gck_part_finish(perm, err)                      every rank gets every result
- *
- * The caller owns the exchange (RCCL all_to_all / all_reduce over xGMI, or any transport), or
- * gck_part_check runs the loop with RCCL inside libgck (below).
- * Union schemas only (no &, -, all()); check-time caveat contexts are not taken. A partitioned
- * engine refuses gck_check_bulk*. A partitioned engine builds its label tables from the rows of its
- * first snapshot as loaded, before it drops the rows other ranks own; after a Watch batch it runs
- * without them (every check through the loop). */
-#define GCK_PART_ENTRY_BYTES 12
-#define GCK_PART_FLAG_BYTES(n) (4 * (size_t)(n) + 1)
+ * Rank r of `world` (one process per GPU) owns the objects with gck_partition_owner(id) == r
+ * (id mod world) and holds only (every ingest path filters — gck_add_tuples*, gck_load_csr,
+ * gck_apply_updates* — after interning, so ids and caveat instances agree on every rank; every
+ * rank reads the whole export / Watch stream, none stores another rank's rows):
+ *   - the relationships of the objects it owns;
+ *   - the schema's hub hierarchy (the userset and wildcard relationships of "hub" relations —
+ *     nested groups, teams — which usersets and arrows point at and which allow no caveat or
+ *     expiration), replicated;
+ *   - the hub relationships of the subjects it owns (their side of the label join).
+ * All ranks then check one batch together — every rank calls with the same items and gets every
+ * result: the label join (a subject's owner sends its slot to the resource's owner, which decides
+ * the check), then an exact-depth level loop over what it left, with intersection, exclusion,
+ * all() and caveats, exchanging frontier entries and join state per level. The exchange goes over
+ * RCCL inside libgck (gck_part_init + gck_part_check) or over the caller's transport
+ * (gck_part_check_with). Check-time caveat contexts are not taken in this mode. A partitioned
+ * engine refuses gck_check_bulk*, lookups and snapshot files. */
 /* Before the first snapshot: this engine is rank `rank` of `world` (1 = not partitioned). */
 int gck_set_partition(gck_engine* e, uint32_t rank, uint32_t world);
 uint32_t gck_partition_owner(uint32_t object_id, uint32_t world);
-int gck_part_begin(gck_engine* e, const gck_item* d_items, size_t n, int64_t now_us, void* stream);
-int gck_part_expand(gck_engine* e, uint64_t* send_counts);
-int gck_part_pack(gck_engine* e, void* d_send, size_t send_cap);
-int gck_part_ingest(gck_engine* e, const void* d_recv, size_t n_recv, void* d_flags);
-int gck_part_resolve(gck_engine* e, const void* d_flags, uint32_t* out_active);
-int gck_part_finish(gck_engine* e, uint8_t* d_out_perm, int32_t* d_out_err);
 
-/* The whole partitioned check inside libgck, exchanging over RCCL (xGMI between the GPUs of a
- * node): the loop above with grouped ncclSend / ncclRecv for the counts and the entries and an
- * in-place ncclAllReduce(MAX) of the flag bytes, no host round trip through the caller per
- * level. Rank 0 makes the id (gck_part_unique_id), the caller hands the same bytes to every rank
- * (any transport: a TCP store, MPI, a file), and each rank — one process per GPU, the engine's
- * device — joins with gck_part_init after gck_set_partition. gck_part_check then takes the place
- * of the begin .. finish sequence; every rank calls it with the same items and gets every
- * result. `stream` orders the batch after the caller's writes of the items (NULL: the legacy
- * default stream). */
-/* The label join over a partitioned graph, before the loop above (labels.inc): the hierarchy
- * labels are replicated, a subject's slot lives with the subject's owner and a resource's slot
- * with the resource's owner. gck_part_join_pack writes, for every check whose subject this rank
- * owns and whose permission has label slots, one GCK_PART_JOIN_RECORD_BYTES record (check index and 3 reserved words,
- * the subject's slot) for the owner of the check's resource, grouped by destination rank in rank
- * order (cap: records); the caller moves them all-to-all (a rank's records for itself included)
- * and gck_part_join_decide decides the received ones into zero-initialised perm / err arrays. An
- * all-reduce MAX of the perm bytes then gives every rank every decided check; the checks still at
- * 0 (undecided: their slots overflowed, another shape, a resource at the depth budget) go through
- * the begin .. finish loop, in batch order on every rank. gck_part_check does all of it over
- * RCCL. */
-#define GCK_PART_JOIN_RECORD_BYTES 80
-int gck_part_join_pack(gck_engine* e, const gck_item* d_items, size_t n, void* d_send, size_t send_cap,
-                       uint64_t* send_counts, void* stream);
-int gck_part_join_decide(gck_engine* e, const gck_item* d_items, size_t n, const void* d_recv, size_t n_recv,
-                         uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
+/* A caller's exchange between the ranks of a partition. Device buffers on the engine's device,
+ * ordered on `stream` (the engine's work before the call is on it; the engine reads `recv` after
+ * the call, on it): the transport may enqueue the transfer there (RCCL) or synchronise the stream
+ * and complete it before returning (a host-staged transport).
+ *   alltoallv: this rank sends send_bytes[d] bytes to rank d and receives recv_bytes[s] bytes
+ *     from rank s; the blocks lie back to back in rank order in `send` and `recv` (the engine
+ *     passes 0 for itself). Both sides know the sizes: the engine exchanges them first.
+ *   allreduce_max_u8: in place, element-wise MAX over the ranks of n bytes.
+ * Each returns 0, or non-zero on failure (the check then fails with GCK_E_DEVICE). */
+typedef struct gck_transport {
+  void* ctx;
+  int (*alltoallv)(void* ctx, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                   const uint64_t* recv_bytes, void* stream);
+  int (*allreduce_max_u8)(void* ctx, void* d_buf, uint64_t n, void* stream);
+} gck_transport;
+
+/* The partitioned check over the caller's transport: n device items (the same on every rank) in,
+ * every result out on every rank (d_out_perm / d_out_err, device). `now_us` 0 = rank 0's clock. */
+int gck_part_check_with(gck_engine* e, const gck_transport* t, const gck_item* d_items, size_t n, int64_t now_us,
+                        uint8_t* d_out_perm, int32_t* d_out_err, void* stream);
+
+/* The same over RCCL inside libgck (xGMI between the GPUs of a node: grouped ncclSend / ncclRecv,
+ * ncclAllReduce). Rank 0 makes the id (gck_part_unique_id), the caller hands the same bytes to
+ * every rank (any transport: a TCP store, MPI, a file), and each rank joins with gck_part_init
+ * after gck_set_partition. */
 #define GCK_PART_UNIQUE_ID_BYTES 128
 int gck_part_unique_id(uint8_t out[GCK_PART_UNIQUE_ID_BYTES]);
 int gck_part_init(gck_engine* e, const uint8_t id[GCK_PART_UNIQUE_ID_BYTES]);

@@ -20,7 +20,7 @@ KERNELS = {
     "void gck::k_label_join<24, 32u>(gck::LjArgs)": [112],
     "void gck::k_label_join<32, 16u>(gck::LjArgs)": [112],
     "void gck::k_label_join<32, 32u>(gck::LjArgs)": [112],
-    "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [328, 128],
+    "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [336, 128],
 }
 
 
