@@ -56,12 +56,12 @@ case "$CMD" in
     GCK_AQL_TIMED=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --host-steps 0 "$@" > "$OUT/kt.json" 2> "$OUT/kt.err"
     GCK_AQL_TIMED=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt1" -o kt1 --output-format csv -- python3 bench.py --no-cpu --host-steps 0 --inflight 1 "$@" > "$OUT/kt1.json" 2> "$OUT/kt1.err"
     echo "kernel trace done"
-    # counter passes launch every kernel through HIP (GCK_AQL=0): the same kernels and bytes, on
-    # queues the profiler's counter collection owns (with the engine's own HSA queues it stalls)
+    # counter passes over the path the bench times: the joins dispatched into the engine's own HSA
+    # queues (aql.inc), one batch at a time; GCK_DEBUG_AQL reports a dispatch that would stall
     SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --no-cpu --host-steps 0 --inflight 1 $*"
-    GCK_AQL=0 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- $SHORT > "$OUT/fetch.json" 2> "$OUT/fetch.err"
+    GCK_DEBUG_AQL=1 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- $SHORT > "$OUT/fetch.json" 2> "$OUT/fetch.err"
     echo "fetch pass done"
-    GCK_AQL=0 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- $SHORT > "$OUT/write.json" 2> "$OUT/write.err"
+    GCK_DEBUG_AQL=1 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- $SHORT > "$OUT/write.json" 2> "$OUT/write.err"
     echo "pmc done"
     python3 tools/traffic_summary.py "$OUT" > "$OUT/traffic.json" || true
     cat "$OUT/traffic.json" || true
