@@ -606,6 +606,18 @@ def main():
         st_solo = eng.stats()
         eng.set_profile(False)
         progress("solo launches done")
+    if args.partitioned and not args.no_profile:
+        # the partitioned join's own kernels timed by their events (k_label_join on one rank;
+        # k_pj_pack + k_pj_decide on several, the exchange between them not included), the
+        # global batch again a few times
+        eng.set_profile(True)
+        eng.reset_stats()
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
+        st_solo = eng.stats()
+        eng.set_profile(False)
+        progress("solo partitioned batches done")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -897,8 +909,30 @@ def main():
                 "achieved_job": round(mixed_alg * args.steps / elapsed / 1e9, 3)}
 
     if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
-        cp, ce, _ = corc.check(prog, tab, host_items, threads=threads)
+        t_c = time.perf_counter()
+        cp, ce, cnt_p = corc.check(prog, tab, host_items, threads=threads)
+        t_c = time.perf_counter() - t_c
         agree = float(((cp == res) & (ce == errs)).mean())
+        if not args.no_cpu and world == 1:
+            cpu = {"value": round(len(host_items) / t_c, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+                   "sample": f"rank 0's {len(host_items)} checks of the timed global batch, the same "
+                             f"{n_tuples / 1e6:.0f}M-tuple graph, C oracle (oracle/check_oracle.c, OpenMP {cpu_note}), "
+                             f"{t_c:.1f}s; every sampled check compared with the GPU result"}
+        if st_solo is not None and st_solo["bundle_launches"] and st_solo["bundle_ms"] > 0:
+            # SURVEY §8d algorithmic bytes of rank 0's checks (the oracle's counting mode), over the
+            # join's kernel time on rank 0 (each rank decides about 1/world of the global batch)
+            ck = corc.count_bfs(prog, tab, host_items, threads=threads)
+            b_alg = 25 * len(host_items) + 8 * ck["rows"] + 4 * ck["edges"]
+            ms_a = st_solo["bundle_ms"] / st_solo["bundle_launches"]
+            achieved = b_alg / (ms_a * 1e-3) / 1e9
+            kname = "k_label_join" if world == 1 else "k_pj_pack + k_pj_decide"
+            roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                    "kernel": f"{kname}: the partitioned label join of one global batch on rank 0, timed by the "
+                              f"kernels' own HIP events (the exchange between them not included)",
+                    "alg_bytes_per_launch": int(b_alg), "mean_launch_ms": round(ms_a, 4),
+                    "alg_counts": {k: int(v) for k, v in ck.items()},
+                    "label_checks_per_batch": round(st_solo["label_checks"] / max(1, st_solo["batches"]), 1)}
 
     if rank == 0:
         line = {

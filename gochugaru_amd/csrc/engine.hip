@@ -1520,8 +1520,10 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
         continue;
       }
       if (h.dev_off && e.part_world > 1) {  // partitioned graph: only the edges this rank keeps (partition.inc)
+        const uint64_t loaded = ne;
         part_filter_device(e, *ds, h, d, ne);
         b.n_edges = ne;
+        e.n_tuples -= std::min<uint64_t>(e.n_tuples, loaded - ne);  // (the engine counts what it holds)
         if (ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
