@@ -107,6 +107,8 @@ struct DeviceSnapshot {
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
   std::vector<uint64_t> lj_key;  // what the label tables were built from (labels.inc: reused while unchanged)
   std::vector<void*> lj_ptrs;    // their arrays (in allocs or hallocs)
+  std::vector<void*> adopt_h;    // arrays of the current snapshot this one takes over at publish
+                                 // (device_publish: contiguous ones move to hallocs, others to allocs)
   uint64_t lj_bytes = 0;
   const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
@@ -1476,13 +1478,17 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 // (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
 // derived structures of unchanged CSRs. Taken-over arrays join the new snapshot's allocation
 // list only on success, so a failure frees nothing the previous snapshot still owns.
-void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
+// device_upload in two steps (a Watch batch builds under the engine's shared lock, beside the
+// checks of the current snapshot, and publishes under the exclusive one): device_build reads the
+// current snapshot e.dev but never changes it — arrays it takes over are listed in `adopted`
+// (pool arrays) and DeviceSnapshot::adopt_h (contiguous ones), and pass to the new snapshot only
+// when device_publish swaps it in.
+static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool delta, std::vector<void*>& adopted) {
   PhaseClock pc(delta ? "relink" : "upload");
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
   Schema& sc = *e.schema;
   auto* ds = new DeviceSnapshot();
-  std::vector<void*> adopted;
   try {
     std::vector<DevCSR> table;
     std::vector<CsrInfo> info;
@@ -1646,6 +1652,24 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
     delete ds;
     throw;
   }
+  return ds;
+}
+
+static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& adopted) {
+  PhaseClock pc("publish");
+  if (!ds->adopt_h.empty() && e.dev) {  // contiguous arrays taken over (label tables)
+    auto& oh = e.dev->hallocs;
+    for (void* q : ds->adopt_h) {
+      auto it = std::find(oh.begin(), oh.end(), q);
+      if (it != oh.end()) {
+        oh.erase(it);
+        ds->hallocs.push_back(q);
+      } else {
+        adopted.push_back(q);  // (a pool array)
+      }
+    }
+    ds->adopt_h.clear();
+  }
   if (!adopted.empty()) {
     std::sort(adopted.begin(), adopted.end());
     adopted.erase(std::unique(adopted.begin(), adopted.end()), adopted.end());
@@ -1681,6 +1705,12 @@ void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
   e.generation = ++g_generations;
   HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
   pc.mark("sync");
+}
+
+void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
+  std::vector<void*> adopted;
+  DeviceSnapshot* ds = device_build(e, csrs, delta, adopted);
+  device_publish(e, ds, adopted);
 }
 
 // ---- workspaces ------------------------------------------------------------------------------

@@ -162,7 +162,8 @@ struct Engine {
   // a rank keeps beyond the rows it owns (part_keep)
   std::vector<char> part_hub_node, part_hub_rel;
   bool device_ready = false;
-  std::shared_mutex mu;  // shared: checks; exclusive: schema/snapshot
+  std::shared_mutex mu;  // shared: checks (and a Watch batch's build); exclusive: schema/snapshot
+  std::mutex writer_mu;  // one writer at a time (gck_api.cpp WriterLock; a Watch batch holds it throughout)
   std::unique_ptr<Schema> schema;
   std::string schema_text;  // as loaded (the snapshot cache is keyed by it)
   std::vector<TypeInterner> interner;
@@ -260,7 +261,20 @@ int device_init(Engine& e);
 // delta: a Watch-batch re-link (delta.inc): derived structures of unchanged CSRs and the
 // previous heights are taken over
 void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta = false);
-void device_apply(Engine& e, const std::vector<UpdateGroup>& groups);
+// A Watch batch (delta.inc) in three steps: build the next snapshot beside the current one's
+// checks (engine lock shared: the current snapshot is only read), then publish it (exclusive:
+// batches in flight finished, membership indexes patched, snapshot swapped), or abort.
+struct WatchBuild {
+  DeviceSnapshot* ds = nullptr;
+  std::vector<void*> adopted, fresh;
+  int64_t tuple_delta = 0;
+  const void* patch_jobs = nullptr;  // the deferred membership-index patch: its job table (device)
+  int n_patch_jobs = 0;
+  uint32_t patch_blocks = 0;
+};
+void device_apply_build(Engine& e, const std::vector<UpdateGroup>& groups, WatchBuild& wb);
+void device_apply_publish(Engine& e, WatchBuild& wb);
+void device_apply_abort(Engine& e, WatchBuild& wb);
 // cav: the call's check-time caveat contexts (CavCall above)
 // Pooled check workspaces (one per batch in flight, at most cfg.workspaces): acquire waits for
 // a free one. Callers take their workspaces BEFORE the engine lock (the holders of busy ones

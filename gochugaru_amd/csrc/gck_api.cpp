@@ -160,6 +160,15 @@ static Schema& need_schema(Engine& e) {
 
 extern "C" {
 
+// What changes the engine's state — schema, snapshot, Watch batches, caveat instances, partition
+// — is serialised by Engine::writer_mu and holds the engine lock exclusively; a Watch batch takes
+// the exclusive lock only to start and to publish its snapshot (apply_updates).
+struct WriterLock {
+  std::lock_guard<std::mutex> w;
+  std::unique_lock<std::shared_mutex> lk;
+  explicit WriterLock(Engine& e) : w(e.writer_mu), lk(e.mu) {}
+};
+
 static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_stats) == 232, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32 && sizeof(gck_update) == 40, "item/tuple/update layout");
@@ -194,7 +203,7 @@ int gck_load_schema(gck_engine* ge, const char* text, size_t len) {
     Engine& e = need(ge);
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null schema text");
     auto sc = compile_schema(std::string(text ? text : "", len));
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     drain_batches(e);
     e.schema = std::move(sc);
     partition_rules(e);
@@ -294,7 +303,7 @@ int gck_reserve_objects(gck_engine* ge, uint16_t type, uint32_t n) {
     Engine& e = need(ge);
     REQUIRE(type < need_schema(e).types.size(), GCK_E_INVALID_ARGUMENT, "bad type");
     REQUIRE(n < GCK_ID_ABSENT, GCK_E_CAPACITY, "too many objects");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     TypeInterner& ti = e.interner[type];
     if (n > ti.count) ti.count = n;
   });
@@ -322,7 +331,7 @@ int gck_add_caveat_instance(gck_engine* ge, const char* name, size_t name_len, c
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(name && out_id, GCK_E_INVALID_ARGUMENT, "null argument");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     *out_id = add_caveat_instance(e, std::string(name, name_len), std::string(json ? json : "", json_len));
   });
 }
@@ -345,7 +354,7 @@ int gck_begin_snapshot(gck_engine* ge, uint64_t revision) {
   return guard([&] {
     Engine& e = need(ge);
     need_schema(e);
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     e.staging = true;
     e.staged_revision = revision;
     e.staged.clear();
@@ -360,7 +369,7 @@ int gck_add_tuples(gck_engine* ge, const gck_tuple* tuples, size_t n) {
     need_schema(e);
     REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
     REQUIRE(n == 0 || tuples, GCK_E_INVALID_ARGUMENT, "null tuples");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     stage_tuples(e, tuples, n);
   });
 }
@@ -371,7 +380,7 @@ int gck_add_tuples_text(gck_engine* ge, const char* text, size_t len) {
     need_schema(e);
     REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     add_tuples_text(e, text, len);
   });
 }
@@ -392,7 +401,7 @@ int gck_load_csr(gck_engine* ge, uint16_t relation, uint16_t subject_type, uint1
     REQUIRE(allowed, GCK_E_INVALID_ARGUMENT, "gck_load_csr: subject kind not allowed by the schema");
     REQUIRE(offsets && (neighbours || !n_edges), GCK_E_INVALID_ARGUMENT, "gck_load_csr: null arrays");
     REQUIRE(n_edges < 0xFFFFFFFFull, GCK_E_CAPACITY, "gck_load_csr: more than 2^32-1 edges in one CSR");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     HostCSR h;
     h.rel = relation;
     h.stype = subject_type;
@@ -428,7 +437,7 @@ int gck_commit_snapshot(gck_engine* ge) {
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     drain_batches(e);
     std::vector<HostCSR> csrs = build_csrs(e);
     device_upload(e, csrs);  // device-pointer CSRs are copied before the caller regains control
@@ -445,7 +454,7 @@ int gck_save_snapshot(gck_engine* ge, const char* path) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(path, GCK_E_INVALID_ARGUMENT, "null path");
-    std::unique_lock<std::shared_mutex> lk(e.mu);  // no Watch batch may move the snapshot meanwhile
+    WriterLock lk(e);  // no Watch batch may move the snapshot meanwhile
     save_snapshot_file(e, path);
   });
 }
@@ -455,7 +464,7 @@ int gck_load_snapshot_file(gck_engine* ge, const char* path) {
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(path, GCK_E_INVALID_ARGUMENT, "null path");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     drain_batches(e);
     load_snapshot_file(e, path);
     ensure_pool(e);
@@ -474,7 +483,7 @@ int gck_revision(gck_engine* ge, uint64_t* out) {
 int gck_set_head_revision(gck_engine* ge, uint64_t revision) {
   return guard([&] {
     Engine& e = need(ge);
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     if (revision > e.head_revision) e.head_revision = revision;  // the head only moves forward
   });
 }
@@ -496,8 +505,13 @@ int gck_device_bytes(gck_engine* ge, uint64_t* out) {
 }
 
 // Watch batch: validated and grouped on the host first (nothing is applied if any update is
-// rejected), then merged on the device (delta.inc). A device failure loses the snapshot.
-static void apply_updates(Engine& e, uint64_t revision, const gck_update* ups, size_t n) {
+// rejected), then merged on the device and the next snapshot derived from it (delta.inc) BESIDE
+// the checks: the engine lock is held shared meanwhile, so checks keep running on the current
+// snapshot; it is taken exclusively again only to finish the batches in flight, patch the
+// membership indexes and swap the snapshot in (device_apply_publish). `lk` (exclusive, with
+// writer_mu held) is released and re-acquired here. A device failure loses the snapshot.
+static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, uint64_t revision, const gck_update* ups,
+                          size_t n) {
   REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
   REQUIRE(revision > e.revision || (n == 0 && revision == e.revision), GCK_E_REVISION,
           "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
@@ -514,15 +528,31 @@ static void apply_updates(Engine& e, uint64_t revision, const gck_update* ups, s
   }
   std::vector<UpdateGroup> groups = group_updates(e, ups, n);
   pc.mark("group");
-  if (groups.empty()) drain_batches(e);  // (device_apply drains otherwise)
-  if (!groups.empty()) {
-    try {
-      device_apply(e, groups);
-      pc.mark("device");
-    } catch (...) {
-      e.committed = false;
-      throw;
-    }
+  if (groups.empty()) {
+    drain_batches(e);
+    e.revision = revision;
+    return;
+  }
+  WatchBuild wb;
+  lk.unlock();
+  try {
+    std::shared_lock<std::shared_mutex> sl(e.mu);  // (checks run on the current snapshot meanwhile)
+    device_apply_build(e, groups, wb);
+  } catch (...) {
+    lk.lock();
+    device_apply_abort(e, wb);
+    e.committed = false;
+    throw;
+  }
+  pc.mark("build");
+  lk.lock();
+  try {
+    device_apply_publish(e, wb);
+    pc.mark("publish");
+  } catch (...) {
+    device_apply_abort(e, wb);
+    e.committed = false;
+    throw;
   }
   e.revision = revision;
 }
@@ -532,10 +562,9 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(n == 0 || updates, GCK_E_INVALID_ARGUMENT, "null updates");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
-    // (read in place: no copy of the batch). Batches in flight are drained once the updates are
-    // validated, grouped and staged (delta.inc device_apply): that host work runs beside them
-    apply_updates(e, revision, updates, n);
+    WriterLock wl(e);
+    // (read in place: no copy of the batch)
+    apply_updates(e, wl.lk, revision, updates, n);
   });
 }
 
@@ -582,7 +611,7 @@ int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, 
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock wl(e);
     REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
     // the revision first: a stale batch is refused before its text is read
     REQUIRE(revision > e.revision || (len == 0 && revision == e.revision), GCK_E_REVISION,
@@ -593,9 +622,9 @@ int gck_apply_updates_text(gck_engine* ge, uint64_t revision, const char* text, 
     try {
       std::vector<gck_update> ups;
       parse_updates_text(e, text, len, ups);
-      apply_updates(e, revision, ups.data(), ups.size());
+      apply_updates(e, wl.lk, revision, ups.data(), ups.size());
     } catch (...) {
-      intern_rollback(e, mark);
+      intern_rollback(e, mark);  // (apply_updates returns or throws with the lock held)
       throw;
     }
   });
@@ -799,7 +828,7 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(world >= 1 && world <= 63 && rank < world, GCK_E_INVALID_ARGUMENT, "bad rank / world");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     REQUIRE(!e.committed && !e.dev && e.ws_pool.empty() && !e.part_ws && e.staged.empty() && e.prebuilt.empty(),
             GCK_E_STATE, "gck_set_partition must precede the first snapshot");
     e.part_rank = rank;
@@ -825,7 +854,7 @@ int gck_part_init(gck_engine* ge, const uint8_t* id) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(id, GCK_E_INVALID_ARGUMENT, "null id");
-    std::unique_lock<std::shared_mutex> lk(e.mu);
+    WriterLock lk(e);
     part_init(e, id);
   });
 }
