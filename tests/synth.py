@@ -250,13 +250,16 @@ class NestedChurn:
     def _layer_of(self, g):
         return np.searchsorted(self.layer_start, g, side="right") - 1
 
-    def batch(self, n: int, cycle: bool = False):
+    def batch(self, n: int, cycle: bool = False, share=(0.9, 0.05, 0.05)):
+        """n updates split over memberships / nesting / viewers by `share` (a 0 share: none of
+        that kind, e.g. (0.95, 0, 0.05) leaves the hierarchy as it is)."""
         from gochugaru_amd.engine import UPDATE_CREATE, UPDATE_DELETE, UPDATE_DTYPE, UPDATE_TOUCH
         rng, G = self.rng, self.G
-        share = [0.9, 0.05, 0.05]
         out = []
         for kind, frac in zip(self.KINDS, share):
             rel, st, sr = kind
+            if frac <= 0 and not (cycle and kind == (R_MEMBER, T_GROUP, R_MEMBER)):
+                continue
             k = max(1, int(n * frac))
             keys = self.keys[kind]
             ops = rng.choice([UPDATE_CREATE, UPDATE_TOUCH, UPDATE_DELETE], size=k, p=[0.45, 0.45, 0.10])

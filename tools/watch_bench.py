@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--churn", type=float, default=0.001)
     ap.add_argument("--cycle-at", type=int, default=-1, help="batch index that closes a hierarchy cycle")
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--mix", default="all", choices=["all", "members", "nesting"],
+                    help="all: memberships / nesting / viewers 90/5/5 %%; members: memberships and viewers only "
+                         "(95/0/5: the hierarchy unchanged); nesting: nesting only")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -38,7 +41,7 @@ def main():
     e = load_engine(G)
     print(f"[watch] loaded {G.n_tuples} tuples in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
-    out = {"tuples": G.n_tuples, "churn": args.churn, "batches": []}
+    out = {"tuples": G.n_tuples, "churn": args.churn, "mix": args.mix, "batches": []}
 
     def measure(tag):
         e.reset_stats()
@@ -60,7 +63,8 @@ def main():
     out["batches"].append(measure("initial"))
     n_up = int(G.n_tuples * args.churn)
     for b in range(args.batches):
-        ups = C.batch(n_up, cycle=(b == args.cycle_at))
+        share = {"all": (0.9, 0.05, 0.05), "members": (0.95, 0.0, 0.05), "nesting": (0.0, 1.0, 0.0)}[args.mix]
+        ups = C.batch(n_up, cycle=(b == args.cycle_at), share=share)
         torch.cuda.synchronize()
         t = time.perf_counter()
         e.apply_updates(2 + b, ups)
