@@ -526,20 +526,21 @@ static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, ui
     ups = mine.data();
     n = mine.size();
   }
-  std::vector<UpdateGroup> groups = group_updates(e, ups, n);
-  pc.mark("group");
-  if (groups.empty()) {
-    drain_batches(e);
-    e.revision = revision;
-    return;
-  }
+  // validation and grouping read the interner and the schema, which only writers change (and
+  // writer_mu holds them off): beside the checks too
   WatchBuild wb;
+  std::vector<UpdateGroup> groups;
   lk.unlock();
+  bool built = false;
   try {
     std::shared_lock<std::shared_mutex> sl(e.mu);  // (checks run on the current snapshot meanwhile)
-    device_apply_build(e, groups, wb);
+    groups = group_updates(e, ups, n);
+    pc.mark("group");
+    if (!groups.empty()) device_apply_build(e, groups, wb);
+    built = true;
   } catch (...) {
     lk.lock();
+    if (!built && !wb.ds && wb.fresh.empty()) throw;  // rejected before anything was built: nothing lost
     device_apply_abort(e, wb);
     e.committed = false;
     throw;
