@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-max-batches", type=int, default=400)
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "final", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "aql_pmc", "traffic.json"),
                     help="rocprofv3 PMC HBM bytes per batch (tools/gpu.sh profile, calibrated by tools/gather_probe)")
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None,

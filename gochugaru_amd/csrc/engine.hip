@@ -22,6 +22,7 @@
 #include <cxxabi.h>
 #include <dlfcn.h>
 #include <hip/hip_ext.h>
+#include <hipcub/hipcub.hpp>
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -74,6 +75,27 @@ struct Derived {  // a bidirectional structure and the base CSR it was built fro
   uint32_t* cov_pre = nullptr;
 };
 
+// User slots of the snapshot (bidir.inc slots_for), found again by the next Watch batch, which
+// recomputes only the slots of the users it touched when the hierarchy labels are unchanged.
+struct SlotRec {
+  const uint32_t* src_off;  // the transposed CSR the slots were built over
+  const uint32_t* lab;      // the closure's labels and covers they were built from
+  const uint32_t* cov_pre;
+  uint32_t* slots;
+  uint32_t* list;           // cover lists (null: none)
+  uint64_t list_total;      // entries in `list`
+  uint32_t n_rows;
+};
+
+// Slots of some users, written into a slot array the snapshot shares with the current one when it
+// is published (device_publish, after the batches in flight on the current one have finished).
+struct SlotPatch {
+  uint32_t* slots;
+  const uint32_t* staged;  // kUSlotWords per user, in `ids` order
+  const uint32_t* ids;
+  uint32_t n;
+};
+
 struct DeviceSnapshot {
   std::vector<void*> allocs;
   std::vector<void*> hallocs;  // hipExtMallocWithFlags (physically contiguous) arrays: hipFree
@@ -109,6 +131,8 @@ struct DeviceSnapshot {
   std::vector<void*> lj_ptrs;    // their arrays (in allocs or hallocs)
   std::vector<void*> adopt_h;    // arrays of the current snapshot this one takes over at publish
                                  // (device_publish: contiguous ones move to hallocs, others to allocs)
+  std::vector<SlotRec> slot_recs;
+  std::vector<SlotPatch> slot_patches;  // applied by device_publish
   uint64_t lj_bytes = 0;
   const unsigned char* d_lj = nullptr;
   uint32_t node_bits = 1, q_bits = 1, q_bits_deep = 1;  // query-id bits of the visited keys (make_key)
@@ -118,6 +142,20 @@ struct DeviceSnapshot {
 };
 
 struct PartState;  // partition.inc
+
+// What a Watch batch being built (delta.inc device_apply_build) tells the snapshot build: the
+// transposed CSRs it merged (taken over by build_bidir instead of transposing again), and per
+// merged transpose the users whose memberships changed (slots_for recomputes only theirs).
+struct DeltaHint {
+  std::vector<Derived> derived;
+  struct Users {
+    const uint32_t* t_off;      // the merged transposed CSR
+    const uint32_t* old_t_off;  // the current snapshot's, which it replaces
+    const uint32_t* ids;        // users with a changed membership (device, ascending)
+    uint32_t n;
+  };
+  std::vector<Users> users;
+};
 
 // One check workspace: the scratch of one batch in flight, on its own HIP stream. An engine
 // keeps a pool of them (acquire_ws / release_ws), so concurrent callers — and the batches a
@@ -1657,6 +1695,15 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
 
 static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& adopted) {
   PhaseClock pc("publish");
+  if (!ds->slot_patches.empty()) {  // (the batches in flight on the current snapshot have finished)
+    for (const SlotPatch& sp : ds->slot_patches)
+      if (sp.n)
+        hipLaunchKernelGGL(k_slot_scatter, dim3(grid_for(sp.n)), dim3(kBlock), 0, 0, sp.slots, sp.staged, sp.ids, sp.n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(nullptr));
+    ds->slot_patches.clear();
+    pc.mark("slot_patch");
+  }
   if (!ds->adopt_h.empty() && e.dev) {  // contiguous arrays taken over (label tables)
     auto& oh = e.dev->hallocs;
     for (void* q : ds->adopt_h) {

@@ -216,6 +216,7 @@ struct Engine {
   // direct AQL dispatch of the join kernels (engine.hip aql.inc): the engine's HSA queue and the
   // kernels of libgck_kernels.co, set up at the first snapshot (null: launches go through HIP)
   struct AqlState* aql = nullptr;
+  struct DeltaHint* delta_hint = nullptr;  // set while a Watch batch builds its snapshot (delta.inc)
   bool aql_tried = false;
   ~Engine();
 };
