@@ -903,8 +903,10 @@ def main():
         achieved = mixed_alg / (ms_a * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                "kernel": "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks), "
-                          "HIP events on its launch stream, sampled every 4th batch in the timed region",
+                "kernel": ("stage A of the check batch: k_label_join with the caveat plane, then k_bundles<1> over "
+                           "the checks it deferred" if st["label_checks"] > 0 else
+                           "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks)")
+                          + ", HIP events on its launch stream, sampled every 4th batch in the timed region",
                 "alg_bytes_per_launch": int(mixed_alg), "mean_launch_ms": round(ms_a, 4),
                 "achieved_job": round(mixed_alg * args.steps / elapsed / 1e9, 3)}
 
@@ -996,6 +998,7 @@ def main():
                             "extra_passes_per_step": round(st["caveat_passes"] / args.steps, 2)}}
                if WL.kind == "quota" else {}),
             **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warm + args.steps) * 1e3, 3),
+                          "share_of_step": round(rev["apply_s"] / (args.warm + args.steps) / (elapsed / args.steps), 3),
                           "revision": rev["r"]}} if WL.kind == "mixed" else {}),
         }
         print(json.dumps(line), flush=True)

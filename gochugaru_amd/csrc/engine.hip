@@ -127,8 +127,16 @@ struct DeviceSnapshot {
   std::vector<unsigned char> lj_host;
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
+  bool lj_cav = false;        // some label root holds caveated pairs (labels.inc kLjCav)
   std::vector<uint64_t> lj_key;  // what the label tables were built from (labels.inc: reused while unchanged)
+  std::vector<uint64_t> lj_dkey; // ... of it, the CSRs that feed only the resource slots' user lists
+  std::vector<const uint32_t*> lj_hgt;  // the roots' heights arrays the tables were built against
   std::vector<void*> lj_ptrs;    // their arrays (in allocs or hallocs)
+  // subjects a Watch batch changed a direct grant of since the tables were built (bit per subject;
+  // null: none): their checks go to the wave bundles (labels.inc, lj_dirty_path)
+  uint32_t* lj_dirty = nullptr;
+  uint64_t lj_dirty_n = 0;       // changed grants marked (an upper bound of the dirty subjects)
+  uint32_t lj_users = 0;
   std::vector<void*> adopt_h;    // arrays of the current snapshot this one takes over at publish
                                  // (device_publish: contiguous ones move to hallocs, others to allocs)
   std::vector<SlotRec> slot_recs;
@@ -148,6 +156,15 @@ struct PartState;  // partition.inc
 // merged transpose the users whose memberships changed (slots_for recomputes only theirs).
 struct DeltaHint {
   std::vector<Derived> derived;
+  struct Fwd {  // a merged forward CSR class: its new neighbours and the batch's keys into it
+    const uint32_t* nbr;
+    const unsigned long long* keys;  // (object << 32 | subject), D of them
+    const uint8_t* ins;              // after k_dj_prefix: inserted / removed (0 0: unchanged)
+    const uint8_t* found;
+    uint32_t D;
+    bool wild;  // a wildcard subject among the keys
+  };
+  std::vector<Fwd> fwd;
   struct Users {
     const uint32_t* t_off;      // the merged transposed CSR
     const uint32_t* old_t_off;  // the current snapshot's, which it replaces
@@ -264,6 +281,8 @@ struct Workspace {
   unsigned long long* req_list = nullptr; // kReqCap pairs
   unsigned* req_cnt = nullptr;
   uint8_t* cav_flag = nullptr;  // per check of the batch: its walk touched a pair whose evaluation failed
+  struct Ctx* d_ctx = nullptr;  // the batch's Ctx for the label join's caveated pairs (LjArgs::cx)
+  struct Ctx* h_ctx = nullptr;  // (pinned: its upload is ordered on the batch's stream)
   uint32_t b_cav_req = 0, b_cav_err = 0;  // the published cav_requests / cav_errors of the batch's pass
   // lookups (lookup.inc): matching ids / permissionships of one candidate chunk, their count
   uint32_t* lk_ids = nullptr;
@@ -1375,6 +1394,7 @@ static void free_workspace(Workspace* w) {
   free_list(w->allocs);
   if (w->h_ctr) (void)hipHostFree(w->h_ctr);
   if (w->h_items) (void)hipHostFree(w->h_items);
+  if (w->h_ctx) (void)hipHostFree(w->h_ctx);
   if (w->dbg) (void)hipFree(w->dbg);
   if (w->timing) (void)hipFree(w->timing);
   if (w->ev0) (void)hipEventDestroy(w->ev0);
@@ -1796,6 +1816,8 @@ static Workspace* create_workspace(Engine& e) {
     w->d_perm = dalloc<uint8_t>(w->allocs, w->max_batch, &w->bytes);
     w->d_err = dalloc<int32_t>(w->allocs, w->max_batch, &w->bytes);
     w->cav_flag = dalloc<uint8_t>(w->allocs, w->max_batch, &w->bytes);
+    w->d_ctx = reinterpret_cast<Ctx*>(dalloc<unsigned char>(w->allocs, sizeof(Ctx), &w->bytes));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&w->h_ctx), sizeof(Ctx), hipHostMallocDefault));
     HIP_OK(hipHostMalloc(&w->h_ctr, sizeof(DevCounters) + (kBCtrs + 4) * sizeof(unsigned),
                          hipHostMallocCoherent | hipHostMallocMapped));
     w->h_bctrs = reinterpret_cast<unsigned*>(w->h_ctr + 1);
@@ -2287,6 +2309,12 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.n_fwd = ds.n_fwd;
     j.table_bytes = (uint32_t)((ds.lj_host.size() + 3) & ~(size_t)3);
     j.o_meta = ds.lj_o_meta;
+    j.dirty = ds.lj_dirty;
+    if (ds.lj_cav && w.cav_on) {  // caveated pairs decided under the check contexts (cav_state)
+      *w.h_ctx = c;
+      HIP_OK(hipMemcpyAsync(w.d_ctx, w.h_ctx, sizeof(Ctx), hipMemcpyHostToDevice, st));
+      j.cx = w.d_ctx;
+    }
     if (self_pub) {  // self-published (see the closure join below)
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;

@@ -5,6 +5,7 @@ grants do not fit a slot, cover lists of users in many groups, and what it must 
 bundles (resources at the depth budget, userset subjects, other subject types, cyclic
 hierarchies). Every answer is compared with oracle/spicedb_ref.py, and the label
 path's use is asserted from the engine's counters."""
+import json
 import random
 
 import pytest
@@ -158,3 +159,147 @@ def test_labels_follow_watch_batches():
         got = [(int(p), int(x)) for p, x in zip(perm, err)]
         assert got == want, rev
     e.close()
+
+
+# ---- the caveat plane (BASELINE config 5 shape: caveated grants through folder chains) -------
+
+CAV_PLANE = """
+caveat only_on_tuesday(day_of_the_week string) {
+  day_of_the_week == "tuesday"
+}
+caveat before_2030(now timestamp) {
+  now < timestamp("2030-01-01T00:00:00Z")
+}
+definition user {}
+definition group {
+  relation member: user | group#member
+}
+definition folder {
+  relation parent: folder
+  relation viewer: user | group#member | user with only_on_tuesday
+  relation editor: user | group#member | user with only_on_tuesday | user with before_2030
+  permission edit = editor + parent->edit
+  permission view = viewer + edit + parent->view
+}
+definition doc {
+  relation parent: folder
+  relation owner: user
+  relation viewer: user | user:* | group#member | user with only_on_tuesday | user:* with only_on_tuesday | user with expiration
+  relation banned: user | user with only_on_tuesday
+  relation editor: user | group#member | user with only_on_tuesday
+  permission edit = owner + editor + parent->edit
+  permission view = viewer + edit + parent->view
+  permission strict = view - banned
+  permission both = view & edit
+}
+use expiration
+"""
+
+CAV_CONTEXTS = [None, {"day_of_the_week": "tuesday"}, {"day_of_the_week": "monday"},
+                {"now": "2025-01-01T00:00:00Z"}, {"now": "2031-01-01T00:00:00Z", "day_of_the_week": "tuesday"},
+                {"now": "not a timestamp"}]
+
+
+def _caveat_plane_graph(rng, n_users=60, n_groups=20, n_folders=24, n_docs=120):
+    """Config 5 in small: a folder forest with caveated user grants on every level — a partial
+    caveat, one decided by its stored context alone (true or false), another caveat — nested
+    groups, caveated wildcards and bans, and a few expiring grants (left to the bundles)."""
+    def user_grant():
+        u = f"user:u{rng.randrange(n_users)}"
+        x = rng.random()
+        if x < 0.45:
+            return u
+        if x < 0.75:
+            return u + "[only_on_tuesday]"
+        if x < 0.85:
+            return u + '[only_on_tuesday:{"day_of_the_week":"tuesday"}]'
+        return u + '[only_on_tuesday:{"day_of_the_week":"monday"}]'
+    t = []
+    for g in range(1, n_groups):
+        t.append(f"group:g{g}#member@group:g{rng.randrange(0, g)}#member")
+    for g in range(n_groups):
+        for _ in range(rng.randrange(1, 4)):
+            t.append(f"group:g{g}#member@user:u{rng.randrange(n_users)}")
+    for f in range(1, n_folders):
+        t.append(f"folder:f{f}#parent@folder:f{rng.randrange(max(0, f - 4), f)}")
+    for f in range(n_folders):
+        for _ in range(rng.randrange(0, 4)):
+            t.append(f"folder:f{f}#viewer@{user_grant()}")
+        if rng.random() < 0.3:
+            t.append(f"folder:f{f}#editor@user:u{rng.randrange(n_users)}[before_2030]")
+        if rng.random() < 0.4:
+            t.append(f"folder:f{f}#editor@group:g{rng.randrange(n_groups)}#member")
+    for d in range(n_docs):
+        t.append(f"doc:d{d}#parent@folder:f{rng.randrange(n_folders)}")
+        t.append(f"doc:d{d}#owner@user:u{rng.randrange(n_users)}")
+        for _ in range(rng.randrange(0, 3)):
+            t.append(f"doc:d{d}#viewer@{user_grant()}")
+        if rng.random() < 0.5:
+            t.append(f"doc:d{d}#editor@{user_grant()}")
+        if d % 13 == 0:
+            t.append(f"doc:d{d}#viewer@user:*[only_on_tuesday]")
+        if d % 29 == 0:
+            t.append(f"doc:d{d}#viewer@user:*")
+        if d % 31 == 0:
+            t.append(f"doc:d{d}#viewer@user:u{rng.randrange(n_users)}[expiration:2999-01-01T00:00:00Z]")
+        if rng.random() < 0.3:
+            t.append(f"doc:d{d}#banned@{user_grant()}")
+    checks = [f"doc:d{rng.randrange(n_docs)}#{p}@user:u{rng.randrange(n_users)}"
+              for p in ("view", "edit", "strict", "both") for _ in range(500)]
+    checks += [f"folder:f{rng.randrange(n_folders)}#{p}@user:u{rng.randrange(n_users)}"
+               for p in ("view", "edit") for _ in range(200)]
+    return sorted(set(t)), checks
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_caveat_plane(seed, lazy):
+    """Caveated grants in the label join's slots (labels.inc kLjCav): a term that reaches the
+    subject only through partial caveats is decided by the caveat under the check's context —
+    the dense outcome table, or the lazy (instance, context) map when every check brings its own
+    context — in SpiceDB's tri-state algebra through exclusion and intersection, CONDITIONAL
+    without a context, the item error when the caveat fails to evaluate. Bit-exact against the
+    oracle; nearly every check answered by the label join (resources with an expiring grant are
+    the bundles')."""
+    rng = random.Random(seed)
+    tuples, checks = _caveat_plane_graph(rng)
+    ctxs = [rng.choice(CAV_CONTEXTS) for _ in checks]
+    if lazy:  # distinct contexts: more (instance, context) pairs than the dense table takes
+        ctxs = [dict(c or {}, k=i) for i, c in enumerate(ctxs)]
+    ck = oracle_for(CAV_PLANE, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c), x)) for c, x in zip(checks, ctxs)]
+    e = E.Engine()
+    e.load_schema(CAV_PLANE)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    items = e.make_items([parse_check(c) for c in checks])
+    texts, slots = [], {}
+    for i, x in enumerate(ctxs):
+        if x is None:
+            continue
+        js = json.dumps(x, sort_keys=True)
+        if js not in slots:
+            texts.append(js)
+            slots[js] = len(texts)
+        items[i]["context_slot"] = slots[js]
+    e.reset_stats()
+    perm, err = e.check_bulk(items, now_us=gen.NOW_US, contexts=texts)
+    st = e.stats()
+    e.close()
+    got = [(int(p), int(x)) for p, x in zip(perm, err)]
+    bad = [(c, x, w, g) for c, x, w, g in zip(checks, ctxs, want, got) if w != g]
+    assert not bad, bad[:10]
+    kinds = {w for w in want}
+    assert (3, 0) in kinds and (2, 0) in kinds and (1, 0) in kinds and (0, 6) in kinds, kinds
+    assert st["label_checks"] >= 0.8 * len(checks), (st["label_checks"], len(checks))
+    if lazy:
+        assert st["caveat_passes"] >= 1, st
+
+
+def test_caveat_plane_without_contexts():
+    """No check contexts: a subject reached only through partial caveats is CONDITIONAL; one
+    decided by its stored context alone is a plain grant or none."""
+    rng = random.Random(3)
+    tuples, checks = _caveat_plane_graph(rng)
+    st, want = _run(CAV_PLANE, tuples, checks)
+    assert any(w == (3, 0) for w in want)
+    assert st["label_checks"] >= 0.8 * len(checks), st["label_checks"]
