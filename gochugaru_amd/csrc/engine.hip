@@ -85,6 +85,7 @@ struct SlotRec {
   uint32_t* list;           // cover lists (null: none)
   uint64_t list_total;      // entries in `list`
   uint32_t n_rows;
+  uint8_t kind;             // bidir.inc SlotKind (user / resource slots)
 };
 
 // Slots of some users, written into a slot array the snapshot shares with the current one when it
@@ -1275,7 +1276,9 @@ static T* dalloc(std::vector<void*>& list, size_t count, uint64_t* bytes = nullp
 // batch). At most kRecycleMax bytes are kept; an array is reused for a request of at least 2/3
 // of its size, and allocated with 1/8 of slack so that the next batch's (slightly larger) array
 // fits it.
-constexpr size_t kRecycleMax = (size_t)1 << 30;
+// (The largest CSRs of a 1e9-tuple graph — the group -> user memberships and their transpose, 4-5 GB
+// each — are among them: a fresh allocation of that size costs tens of ms.)
+constexpr size_t kRecycleMax = (size_t)24 << 30;
 
 template <class T>
 static T* ralloc(Engine& e, std::vector<void*>& list, size_t count) {
@@ -2324,12 +2327,14 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.coherent = coherent;
       w.b_seq = j.seq;
     }
-    static const char* const lj_names[4] = {"void gck::k_label_join<24, 16u>(gck::LjArgs)",
-                                            "void gck::k_label_join<24, 32u>(gck::LjArgs)",
-                                            "void gck::k_label_join<32, 16u>(gck::LjArgs)",
-                                            "void gck::k_label_join<32, 32u>(gck::LjArgs)"};
-    const int v = (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
-    if (!aql_try(lj_names[v], &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves)))
+    static const char* const lj_names[8] = {
+        "void gck::k_label_join<24, 16u, 32u>(gck::LjArgs)", "void gck::k_label_join<24, 16u, 16u>(gck::LjArgs)",
+        "void gck::k_label_join<24, 32u, 32u>(gck::LjArgs)", "void gck::k_label_join<24, 32u, 16u>(gck::LjArgs)",
+        "void gck::k_label_join<32, 16u, 32u>(gck::LjArgs)", "void gck::k_label_join<32, 16u, 16u>(gck::LjArgs)",
+        "void gck::k_label_join<32, 32u, 32u>(gck::LjArgs)", "void gck::k_label_join<32, 32u, 16u>(gck::LjArgs)"};
+    const uint32_t cpw = lj_cpw();
+    const int v = (ds.lj_bits == 24 ? 0 : 4) + (ds.lj_sw == 16 ? 0 : 2) + (cpw == 16 ? 1 : 0);
+    if (!aql_try(lj_names[v], &j, sizeof(j), (n + cpw * kWaves - 1) / (cpw * kWaves)))
       lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
   } else if (cj) {
     CjArgs j{};

@@ -71,3 +71,21 @@ def test_positive_half_at_scale():
     perm, err = run(e, items)
     assert np.all(err == 0) and np.all(perm == 2)
     e.close()
+
+
+@pytest.mark.parametrize("layers", [80, 400])
+def test_deep_hierarchy_device_closure(layers):
+    """The ancestor closure, tree labels and covers built on the device level by level
+    (ancestors.inc): hundreds of nesting layers over 160K groups, so a level relaxation pass
+    carries changes down many layers at once (blocks run in id order, parents precede their
+    children) — every level must still be built. Bit-exact against the C oracle."""
+    G = synth.build(2e7, device="cuda", layers=layers)
+    e = load_engine(G)
+    items = synth.checks(G, 65536, seed=23)
+    perm, err = run(e, items)
+    e.close()
+    _, prog, tab = _oracle(G)
+    cp, ce, _ = corc.check(prog, tab, items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1), threads=16)
+    assert np.array_equal(err, ce)
+    mism = np.nonzero(perm != cp)[0]
+    assert mism.size == 0, (mism[:10], perm[mism[:10]], cp[mism[:10]])
