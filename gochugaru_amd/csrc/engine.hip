@@ -129,6 +129,7 @@ struct DeviceSnapshot {
   uint32_t lj_o_meta = 0, lj_sw = 0, lj_bits = 24;
   bool lj_preferred = false;  // the labels cover every closure-join root and more: they take stage A
   bool lj_cav = false;        // some label root holds caveated pairs (labels.inc kLjCav)
+  uint32_t n_cav = 0;         // caveat instances in cav_static / cav_row
   std::vector<uint64_t> lj_key;  // what the label tables were built from (labels.inc: reused while unchanged)
   std::vector<uint64_t> lj_dkey; // ... of it, the CSRs that feed only the resource slots' user lists
   std::vector<const uint32_t*> lj_hgt;  // the roots' heights arrays the tables were built against
@@ -1696,6 +1697,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
     ds->csrs = reinterpret_cast<DevCSR*>(d_blob + o_csrs);
     ds->type_counts = reinterpret_cast<uint32_t*>(d_blob + o_counts);
     ds->cav_static = d_blob + o_cst;
+    ds->n_cav = (uint32_t)cst.size();
     ds->cav_row = reinterpret_cast<uint32_t*>(d_blob + o_crow);
     ds->d_hgt = reinterpret_cast<const unsigned long long*>(d_blob + o_hgt);
     ds->d_cj = ds->cj_host.empty() ? nullptr : d_blob + o_cj;
@@ -2313,10 +2315,17 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.table_bytes = (uint32_t)((ds.lj_host.size() + 3) & ~(size_t)3);
     j.o_meta = ds.lj_o_meta;
     j.dirty = ds.lj_dirty;
+    bool cl = false;
     if (ds.lj_cav && w.cav_on) {  // caveated pairs decided under the check contexts (cav_state)
       *w.h_ctx = c;
       HIP_OK(hipMemcpyAsync(w.d_ctx, w.h_ctx, sizeof(Ctx), hipMemcpyHostToDevice, st));
       j.cx = w.d_ctx;
+      // the dense outcome table and the instances in LDS when they fit (labels.inc LjCavLds)
+      const uint32_t rows = w.cav.n_dist ? (uint32_t)(w.cav.dense.size() / w.cav.n_dist) : 0u;
+      cl = !w.cav_lazy && ds.n_cav <= kLjCavInst && w.cav.dense.size() <= kLjCavDense && w.cav.n_ctx <= kLjCavCtx &&
+           w.cav.n_dist <= 255 && rows < 0xFFFFu;
+      j.cav_n = ds.n_cav;
+      j.cav_rows = rows;
     }
     if (self_pub) {  // self-published (see the closure join below)
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
@@ -2328,14 +2337,14 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       w.b_seq = j.seq;
     }
     static const char* const lj_names[8] = {
-        "void gck::k_label_join<24, 16u, 32u>(gck::LjArgs)", "void gck::k_label_join<24, 16u, 16u>(gck::LjArgs)",
-        "void gck::k_label_join<24, 32u, 32u>(gck::LjArgs)", "void gck::k_label_join<24, 32u, 16u>(gck::LjArgs)",
-        "void gck::k_label_join<32, 16u, 32u>(gck::LjArgs)", "void gck::k_label_join<32, 16u, 16u>(gck::LjArgs)",
-        "void gck::k_label_join<32, 32u, 32u>(gck::LjArgs)", "void gck::k_label_join<32, 32u, 16u>(gck::LjArgs)"};
+        "void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<24, 16u, 16u, false>(gck::LjArgs)",
+        "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<24, 32u, 16u, false>(gck::LjArgs)",
+        "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<32, 16u, 16u, false>(gck::LjArgs)",
+        "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<32, 32u, 16u, false>(gck::LjArgs)"};
     const uint32_t cpw = lj_cpw();
     const int v = (ds.lj_bits == 24 ? 0 : 4) + (ds.lj_sw == 16 ? 0 : 2) + (cpw == 16 ? 1 : 0);
-    if (!aql_try(lj_names[v], &j, sizeof(j), (n + cpw * kWaves - 1) / (cpw * kWaves)))
-      lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr);
+    if (cl || !aql_try(lj_names[v], &j, sizeof(j), (n + cpw * kWaves - 1) / (cpw * kWaves)))
+      lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr, cl);
   } else if (cj) {
     CjArgs j{};
     j.items = d_items;
