@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-labels", action="store_true",
+                    help="engine without the label-join stage (GCK_FLAG_NO_LABELS): the A/B of the join")
     ap.add_argument("--cpu-max-batches", type=int, default=400)
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "aql_pmc", "traffic.json"),
@@ -360,6 +362,7 @@ def main():
     # events only for the solo phase after the timed region (and the configs timed without one)
     solo_profile = WL.kind not in ("mixed", "quota") and not args.partitioned
     eng = Engine(device=local, profile=not args.no_profile and not solo_profile, workspaces=max(2, depth),
+                 labels=not args.no_labels,
                  max_batch=args.batch * world if args.partitioned else args.batch, wide_only=args.wide_only,
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,

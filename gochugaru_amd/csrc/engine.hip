@@ -2336,14 +2336,12 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.coherent = coherent;
       w.b_seq = j.seq;
     }
-    static const char* const lj_names[8] = {
-        "void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<24, 16u, 16u, false>(gck::LjArgs)",
-        "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<24, 32u, 16u, false>(gck::LjArgs)",
-        "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<32, 16u, 16u, false>(gck::LjArgs)",
-        "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)", "void gck::k_label_join<32, 32u, 16u, false>(gck::LjArgs)"};
-    const uint32_t cpw = lj_cpw();
-    const int v = (ds.lj_bits == 24 ? 0 : 4) + (ds.lj_sw == 16 ? 0 : 2) + (cpw == 16 ? 1 : 0);
-    if (cl || !aql_try(lj_names[v], &j, sizeof(j), (n + cpw * kWaves - 1) / (cpw * kWaves)))
+    static const char* const lj_names[4] = {"void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)",
+                                            "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)"};
+    const int v = (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
+    if (cl || !aql_try(lj_names[v], &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves)))
       lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr, cl);
   } else if (cj) {
     CjArgs j{};
