@@ -939,6 +939,36 @@ def main():
                     "alg_counts": {k: int(v) for k, v in ck.items()},
                     "label_checks_per_batch": round(st_solo["label_checks"] / max(1, st_solo["batches"]), 1)}
 
+    check_stage = None
+    if rank == 0 and WL.kind == "mixed":
+        # the check stage alone, after the timed region (never `value`): the timed batch again on the
+        # final snapshot, no Watch batch between, `depth` batches in flight on the engine's streams
+        # with the same contexts — what the one-round join and its leftovers sustain
+        n_cs = 200
+        cs_out = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
+                   torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(depth)]
+        torch.cuda.synchronize()
+        eng.reset_stats()
+        t_cs = time.perf_counter()
+        pend = []
+        for k in range(n_cs):
+            if len(pend) == depth:
+                pend.pop(0).wait()
+            o = cs_out[k % depth]
+            pend.append(eng.submit(items.data_ptr(), args.batch, o[0].data_ptr(), o[1].data_ptr(), device=True,
+                                   engine_stream=True, contexts=m_ctx))
+        for b in pend:
+            b.wait()
+        torch.cuda.synchronize()
+        t_cs = time.perf_counter() - t_cs
+        st_cs = eng.stats()
+        same = all(bool((o[0].cpu() == perm.cpu()).all()) for o in cs_out)
+        check_stage = {"value": round(n_cs * args.batch / t_cs, 1), "unit": "checks/s", "batches": n_cs,
+                       "inflight": depth, "label_checks_per_batch": round(st_cs["label_checks"] / n_cs, 1),
+                       "same_results_as_timed_batch": same,
+                       "note": "the timed batch repeated on the final snapshot without Watch batches between, "
+                               "device-resident, engine streams; not the step"}
+        progress("check-stage phase done")
     if rank == 0:
         line = {
             "metric": ("permission checks/sec (whole node) at batch 64K, 1B tuples" if WL.kind == "nested" else
@@ -1003,6 +1033,7 @@ def main():
             **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_s"] / (args.warm + args.steps) * 1e3, 3),
                           "share_of_step": round(rev["apply_s"] / (args.warm + args.steps) / (elapsed / args.steps), 3),
                           "revision": rev["r"]}} if WL.kind == "mixed" else {}),
+            **({"check_stage": check_stage} if check_stage else {}),
         }
         print(json.dumps(line), flush=True)
     eng.close()
