@@ -2342,7 +2342,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
                                             "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)"};
     const int v = (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
     if (cl || !aql_try(lj_names[v], &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves)))
-      lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed ? w.ev1 : nullptr, cl);
+      lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed && !w.b_chained ? w.ev1 : nullptr, cl);
   } else if (cj) {
     CjArgs j{};
     j.items = d_items;
@@ -2379,7 +2379,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     const bool fast = ds.slot_bits == 24 && small;
     const uint32_t cpw = fast ? 32u : 64u;
     const dim3 grid((n + cpw * kWaves - 1) / (cpw * kWaves)), block(kBlock);
-    hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed ? w.ev1 : nullptr;
+    // (a timed batch with chained bundles stops its clock after them: stage A is both)
+    hipEvent_t e0 = w.b_timed ? w.ev0 : nullptr, e1 = w.b_timed && !w.b_chained ? w.ev1 : nullptr;
     struct {
       Ctx c;
       CjArgs j;
@@ -2407,6 +2408,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     b.idx = w.c_deferred;
     b.n_dev = w.b_ctrs + 4;
     launch_wave_bundles(e, w, c, b, st);
+    if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
   }
   if (host_out) {
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
