@@ -282,9 +282,9 @@ def test_compiled_submit_loop(engine_streams):
 def test_engine_stream_results_read_right_after_wait(family):
     """A device batch on the engine's stream has no caller stream to order reads after: the
     results a caller reads on another stream the moment gck_check_wait returns — no
-    synchronisation with the engine's stream — are the final ones (k_publish after the join, or,
-    under GCK_COHERENT_PUBLISH=1, write-through results published by the join's last block).
-    48 batches over poisoned buffers, 3 in flight."""
+    synchronisation with the engine's stream — are the final ones (the AQL packet's release fence
+    and completion signal, or k_publish after a HIP-launched join). 48 batches over poisoned
+    buffers, 3 in flight."""
     import torch
     schema, tuples, checks = getattr(gen, family)(3)
     e = _engine(schema, tuples, workspaces=3)
@@ -388,3 +388,60 @@ def test_pinned_array_outlives_close():
     import gc
     gc.collect()
     assert e._h is None
+
+
+_KNOB_PROBE = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from gochugaru_amd import engine as E
+from tests import gen
+from tests.helpers import oracle_for, parse_check, to_oracle_item
+schema, tuples, checks = gen.nested(4)
+e = E.Engine(device=0, profile=True, workspaces=3)
+e.load_schema(schema)
+e.load_snapshot_text(1, "\n".join(tuples))
+items = e.make_items([parse_check(c) for c in checks])
+ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+import torch
+n = len(items)
+d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+ok = True
+for _ in range(8):  # device batches on the engine's streams: the AQL path when it is on
+    perm = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    e.submit(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us=gen.NOW_US, device=True,
+             engine_stream=True).wait()
+    ok &= [(int(p), int(x)) for p, x in zip(perm.cpu().numpy(), err.cpu().numpy())] == want
+st = e.stats()
+print(json.dumps({{"ok": ok, "aql_batches": int(st["aql_batches"]), "bundle_ms": float(st["bundle_ms"]),
+                  "launches": int(st["bundle_launches"])}}))
+"""
+
+
+@pytest.mark.parametrize("knob", ["GCK_AQL=0", "GCK_AQL_TIMED=0", ""])
+def test_launch_path_knobs(knob):
+    """The engine's two launch-path knobs, each in a process of its own (read once):
+    GCK_AQL=0 sends every join through HIP, GCK_AQL_TIMED=0 only the profiled (timed) ones;
+    results equal the oracle's either way, and the profiled batches are timed."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    if knob:
+        k, v = knob.split("=")
+        env[k] = v
+    r = subprocess.run([sys.executable, "-c", _KNOB_PROBE.format(root=root)], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"], out
+    assert out["launches"] > 0 and out["bundle_ms"] > 0, out
+    has_co = os.path.exists(os.path.join(os.path.dirname(E.__file__), "libgck_kernels.co"))
+    if knob == "GCK_AQL=0":
+        assert out["aql_batches"] == 0, out
+    elif has_co:
+        assert out["aql_batches"] > 0, out
