@@ -214,6 +214,7 @@ struct Workspace {
   bool aql_devargs = false;     // ... in VRAM (aql.inc AqlState::devargs)
   uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
   void* aql_queue = nullptr;    // aql.inc: the engine queue this workspace dispatches into
+  alignas(16) unsigned char aql_shadow[1024] = {};  // aql.inc: what the kernarg block holds now
   uint64_t n_batches = 0;     // batches run on this workspace (event sampling)
   unsigned b_seq = 0;         // publish sequence of stage A
   float b_ms = 0.f;

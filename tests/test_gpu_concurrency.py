@@ -398,6 +398,7 @@ from gochugaru_amd import engine as E
 from tests import gen
 from tests.helpers import oracle_for, parse_check, to_oracle_item
 schema, tuples, checks = gen.nested(4)
+checks = checks[:400]  # (doc#view@user only: the closure join answers them all, nothing is chained)
 e = E.Engine(device=0, profile=True, workspaces=3)
 e.load_schema(schema)
 e.load_snapshot_text(1, "\n".join(tuples))
@@ -408,7 +409,7 @@ import torch
 n = len(items)
 d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
 ok = True
-for _ in range(8):  # device batches on the engine's streams: the AQL path when it is on
+for _ in range(12):  # device batches on the engine's streams: the AQL path when it is on
     perm = torch.zeros(n, dtype=torch.uint8, device="cuda")
     err = torch.zeros(n, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
