@@ -398,7 +398,6 @@ from gochugaru_amd import engine as E
 from tests import gen
 from tests.helpers import oracle_for, parse_check, to_oracle_item
 schema, tuples, checks = gen.nested(4)
-checks = checks[:400]  # (doc#view@user only: the closure join answers them all, nothing is chained)
 e = E.Engine(device=0, profile=True, workspaces=3)
 e.load_schema(schema)
 e.load_snapshot_text(1, "\n".join(tuples))
@@ -409,7 +408,7 @@ import torch
 n = len(items)
 d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
 ok = True
-for _ in range(12):  # device batches on the engine's streams: the AQL path when it is on
+for _ in range(8):  # device batches on the engine's streams: the AQL path when it is on
     perm = torch.zeros(n, dtype=torch.uint8, device="cuda")
     err = torch.zeros(n, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
@@ -422,27 +421,29 @@ print(json.dumps({{"ok": ok, "aql_batches": int(st["aql_batches"]), "bundle_ms":
 """
 
 
-@pytest.mark.parametrize("knob", ["GCK_AQL=0", "GCK_AQL_TIMED=0", ""])
-def test_launch_path_knobs(knob):
+def test_launch_path_knobs():
     """The engine's two launch-path knobs, each in a process of its own (read once):
     GCK_AQL=0 sends every join through HIP, GCK_AQL_TIMED=0 only the profiled (timed) ones;
-    results equal the oracle's either way, and the profiled batches are timed."""
+    results equal the oracle's either way, and the profiled batches are timed. (The probe's batches
+    leave checks to the bundles, so after the first one every join is chained and launched through
+    HIP: the first batch, profiled, is the one the knobs move.)"""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ)
-    if knob:
-        k, v = knob.split("=")
-        env[k] = v
-    r = subprocess.run([sys.executable, "-c", _KNOB_PROBE.format(root=root)], capture_output=True, text=True,
-                       timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["ok"], out
-    assert out["launches"] > 0 and out["bundle_ms"] > 0, out
-    has_co = os.path.exists(os.path.join(os.path.dirname(E.__file__), "libgck_kernels.co"))
-    if knob == "GCK_AQL=0":
-        assert out["aql_batches"] == 0, out
-    elif has_co:
-        assert out["aql_batches"] > 0, out
+    outs = {}
+    for knob in ["GCK_AQL=0", "GCK_AQL_TIMED=0", ""]:
+        env = dict(os.environ)
+        if knob:
+            k, v = knob.split("=")
+            env[k] = v
+        r = subprocess.run([sys.executable, "-c", _KNOB_PROBE.format(root=root)], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, (knob, r.stderr[-3000:])
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out["ok"], (knob, out)
+        assert out["launches"] > 0 and out["bundle_ms"] > 0, (knob, out)
+        outs[knob] = out["aql_batches"]
+    assert outs["GCK_AQL=0"] == 0, outs
+    if os.path.exists(os.path.join(os.path.dirname(E.__file__), "libgck_kernels.co")):
+        assert outs[""] > outs["GCK_AQL_TIMED=0"], outs
