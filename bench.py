@@ -426,7 +426,7 @@ def main():
         from gochugaru_amd.engine import Contexts
         n_up = max(1, int(n_tuples * args.churn))
         batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warm + args.steps)]
-        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "pending": None}
+        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "pending": None}
         m_ctx = Contexts(CONTEXTS)
 
         def step():
@@ -440,7 +440,9 @@ def main():
                            stream=stream, contexts=m_ctx)
             rev["submit_s"] += time.perf_counter() - t_s
             if rev["pending"] is not None:
+                t_w = time.perf_counter()
                 rev["pending"].wait()  # (already finished by the apply above)
+                rev["wait_s"] += time.perf_counter() - t_w
             rev["pending"] = b
 
         def drain():
@@ -543,7 +545,7 @@ def main():
         trace = np.zeros(2 * args.steps, dtype=np.float64)
         _driver().gckd_set_trace(trace.ctypes.data_as(ctypes.c_void_p), args.steps)
     if WL.kind == "mixed":
-        rev["apply_s"] = rev["submit_s"] = 0.0  # (the Watch share is of the timed steps only)
+        rev["apply_s"] = rev["submit_s"] = rev["wait_s"] = 0.0  # (the Watch share is of the timed steps only)
     t0 = time.perf_counter()
     if native:
         run_steps(args.steps)
@@ -557,7 +559,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if WL.kind == "mixed":
-        rev["apply_timed"], rev["submit_timed"] = rev["apply_s"], rev["submit_s"]
+        rev["apply_timed"], rev["submit_timed"], rev["wait_timed"] = rev["apply_s"], rev["submit_s"], rev["wait_s"]
     if trace is not None:
         _driver().gckd_set_trace(None, 0)
     progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms"
@@ -1039,6 +1041,7 @@ def main():
             **({"watch": {"updates_per_step": n_up, "apply_ms_per_step": round(rev["apply_timed"] / args.steps * 1e3, 3),
                           "share_of_step": round(rev["apply_timed"] / elapsed, 3),
                           "check_submit_ms_per_step": round(rev["submit_timed"] / args.steps * 1e3, 3),
+                          "check_wait_ms_per_step": round(rev["wait_timed"] / args.steps * 1e3, 3),
                           "revision": rev["r"]}} if WL.kind == "mixed" else {}),
             **({"check_stage": check_stage} if check_stage else {}),
         }

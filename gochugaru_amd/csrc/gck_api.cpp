@@ -563,9 +563,15 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
     Engine& e = need(ge);
     need_schema(e);
     REQUIRE(n == 0 || updates, GCK_E_INVALID_ARGUMENT, "null updates");
-    WriterLock wl(e);
-    // (read in place: no copy of the batch)
-    apply_updates(e, wl.lk, revision, updates, n);
+    PhaseClock pc("watch_call");
+    {
+      WriterLock wl(e);
+      pc.mark("lock");
+      // (read in place: no copy of the batch)
+      apply_updates(e, wl.lk, revision, updates, n);
+      pc.mark("apply");
+    }
+    pc.mark("unlock");
   });
 }
 

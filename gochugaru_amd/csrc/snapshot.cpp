@@ -406,30 +406,55 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
   }
   pc.mark("scatter");
   std::vector<UpdateGroup> out(G);
-  uint32_t cnt[2049];
+  std::vector<uint32_t> cnt;
   for (size_t gi = 0; gi < G; ++gi) {
     const size_t lo = start[gi], hi = start[gi + 1];
-    uint64_t orv = 0, andv = ~0ull;
+    // stable sort by key (a later write of a key stays after the earlier ones): one counting pass
+    // on the key's top bits into ~one bucket per update, then an insertion sort of each bucket
+    // (a bucket that a skewed batch fills — many subjects of one object — is merge-sorted)
+    uint64_t kmin = ~0ull, kmax = 0;
     for (size_t i = lo; i < hi; ++i) {
-      orv |= a[i].k;
-      andv &= a[i].k;
+      kmin = std::min(kmin, a[i].k);
+      kmax = std::max(kmax, a[i].k);
     }
     KI* src = a;
-    KI* dst = b;
-    for (int sh = 0; sh < 64; sh += 11) {
-      if ((((orv ^ andv) >> sh) & 2047) == 0) continue;  // constant digit
-      std::memset(cnt, 0, sizeof cnt);
-      for (size_t i = lo; i < hi; ++i) ++cnt[((src[i].k >> sh) & 2047) + 1];
-      for (int j = 0; j < 2048; ++j) cnt[j + 1] += cnt[j];
-      for (size_t i = lo; i < hi; ++i) dst[lo + cnt[(src[i].k >> sh) & 2047]++] = src[i];
-      std::swap(src, dst);
+    const size_t m = hi - lo;
+    if (m > 1 && kmax != kmin) {
+      int lb = 1;
+      while (lb < 16 && ((size_t)1 << lb) < m) ++lb;
+      const int bits = 64 - __builtin_clzll(kmax - kmin);
+      const int sh = bits > lb ? bits - lb : 0;
+      const size_t nb = ((kmax - kmin) >> sh) + 1;
+      cnt.assign(nb + 1, 0u);
+      for (size_t i = lo; i < hi; ++i) ++cnt[((a[i].k - kmin) >> sh) + 1];
+      for (size_t j = 0; j < nb; ++j) cnt[j + 1] += cnt[j];
+      for (size_t i = lo; i < hi; ++i) b[lo + cnt[(a[i].k - kmin) >> sh]++] = a[i];
+      src = b;
+      // (cnt[j] is now the end of bucket j)
+      size_t s0 = lo;
+      for (size_t j = 0; j < nb; ++j) {
+        const size_t s1 = lo + cnt[j];
+        if (s1 - s0 > 32) {
+          std::stable_sort(b + s0, b + s1, [](const KI& x, const KI& y) { return x.k < y.k; });
+        } else {
+          for (size_t i = s0 + 1; i < s1; ++i) {
+            const KI v = b[i];
+            size_t p = i;
+            while (p > s0 && b[p - 1].k > v.k) {
+              b[p] = b[p - 1];
+              --p;
+            }
+            b[p] = v;
+          }
+        }
+        s0 = s1;
+      }
     }
     const uint64_t kind = kinds[by_kind[gi]];
     UpdateGroup& g = out[gi];
     g.rel = (uint16_t)(kind >> 32);
     g.stype = (uint16_t)(kind >> 16);
     g.srel = (uint16_t)kind;
-    const size_t m = hi - lo;
     g.keys.resize(m);
     g.upsert.resize(m);
     g.is_ext.resize(m);

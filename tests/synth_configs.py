@@ -374,7 +374,14 @@ class Mixed:
             t["caveat"] = np.where(ucav & up, cav_instance, 0)
             u["tuple"] = t
             out.append(u)
-        return np.concatenate(out)
+        # (filled in place: np.concatenate would return the records packed, without the padding
+        # UPDATE_DTYPE has, and the engine call would then convert them field by field)
+        res = np.empty(sum(u.size for u in out), dtype=UPDATE_DTYPE)
+        at = 0
+        for u in out:
+            res[at:at + u.size] = u
+            at += u.size
+        return res
 
     # ---- expected answers ------------------------------------------------------------------------
     def expected(self, items_host: np.ndarray, threads: int = 16, stats: dict = None):

@@ -210,3 +210,33 @@ def test_binary_updates_and_index_rebuild():
     assert e.tuple_count == len(store)
     assert e.device_bytes < 3 * bytes0  # merged arrays replace the old ones (no leak)
     e.close()
+
+
+def test_skewed_batch_on_one_object():
+    """A batch whose updates crowd onto a few objects (hundreds of subjects of one group, writes of
+    the same relationship repeated inside the batch): the grouping's bucketed sort keeps every key
+    in order and the last write of each relationship (snapshot.cpp group_updates)."""
+    schema, tuples, checks = gen.nested(3)
+    e = E.Engine()
+    e.load_schema(schema)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    store = {}
+    apply_to_store(store, [("CREATE", t) for t in tuples])
+    rng = random.Random(11)
+    for rnd in range(3):
+        ups = []
+        for k in rng.sample(range(200), 150):  # one object, many subjects (users u0..u199)
+            ups.append(("CREATE", f"group:g{rnd}#member@user:u{k}"))
+        tail = [("DELETE", f"group:g{rnd}#member@user:u{k}") for k in rng.sample(range(200), 100)]
+        tail += [("TOUCH", f"group:g{rnd}#member@user:u{k}") for k in rng.sample(range(200), 60)]  # third writes
+        tail += [(rng.choice(["CREATE", "DELETE"]), f"group:g{rnd + 10}#member@user:u{rng.randrange(200)}")
+                 for _ in range(40)]  # a second object interleaved
+        rng.shuffle(tail)
+        ups += tail
+        e.apply_updates_text(2 + rnd, "\n".join(f"{op} {line}" for op, line in ups))
+        apply_to_store(store, ups)
+        probe = checks + [f"group:g{rnd}#member@user:u{k}" for k in range(200)] + \
+            [f"group:g{rnd + 10}#member@user:u{k}" for k in range(200)]
+        assert engine_results(e, probe) == oracle_results(schema, store, probe), rnd
+    assert e.tuple_count == len(store)
+    e.close()
