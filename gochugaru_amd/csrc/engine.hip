@@ -2247,6 +2247,12 @@ static void launch_wave_bundles(Engine& e, Workspace& w, const Ctx& c, const Bun
 // Stage A of a bundle batch (n <= max_batch): the persistent wave-bundle kernel over every
 // check, then — for a host batch — the copy of the results into the pinned staging, and the
 // publication the host spins on. Nothing waits here.
+// Stage A of a batch begins with the label join (labels.inc) rather than the closure join.
+static bool label_join_on(const Engine& e) {
+  const DeviceSnapshot& ds = *e.dev;
+  return ds.d_lj && (!(ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE)) || ds.lj_preferred);
+}
+
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   Ctx c = make_ctx(e, w, now_us);
@@ -2265,8 +2271,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // launches: the join and the publication
   const DeviceSnapshot& ds = *e.dev;
   const bool cj_ok = ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE);
-  const bool lj = ds.d_lj && (!cj_ok || ds.lj_preferred);
+  const bool lj = label_join_on(e);
   const bool cj = cj_ok && !lj;
+  // the checks' caveat flags start cleared: by the label join with the caveat plane itself (an AQL
+  // dispatch is not ordered after this stream's work), else here
+  if (w.cav_on && !(lj && ds.lj_cav)) HIP_OK(hipMemsetAsync(w.cav_flag, 0, n, st));
   w.b_closure = cj || lj;
   w.b_label = lj;
   // chained: the wave bundles over the join's deferred list follow it in stage A, reading the
@@ -2287,8 +2296,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // the queues they are not the packet's own: GCK_AQL_TIMED=0 launches profiled batches through
   // HIP, timed by their events)
   static const bool aql_timed = !(getenv("GCK_AQL_TIMED") && atoi(getenv("GCK_AQL_TIMED")) == 0);
+  // (a batch with check contexts: the label join with the caveat plane, whose Ctx travels in the
+  // kernarg block and which clears the checks' caveat flags itself — nothing on the HIP stream)
   const bool aql_ok = w.b_own_stream && !host_out && !w.b_chained && ctr_was_clean && e.aql &&
-                      w.aql_kernarg && !w.cav_on && (lj || cj) && (aql_timed || !w.b_timed);
+                      w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
+                      (aql_timed || !w.b_timed);
   w.b_aql = false;
   const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok);
   const uint32_t coherent = 0u;  // (results are published by the kernel end's write-back)
@@ -2317,10 +2329,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.lj_o_meta;
     j.dirty = ds.lj_dirty;
     bool cl = false;
-    if (ds.lj_cav && w.cav_on) {  // caveated pairs decided under the check contexts (cav_state)
-      *w.h_ctx = c;
-      HIP_OK(hipMemcpyAsync(w.d_ctx, w.h_ctx, sizeof(Ctx), hipMemcpyHostToDevice, st));
-      j.cx = w.d_ctx;
+    const bool cav = ds.lj_cav && w.cav_on;  // caveated pairs decided under the check contexts (cav_state)
+    if (cav) {
       // the dense outcome table and the instances in LDS when they fit (labels.inc LjCavLds)
       const uint32_t rows = w.cav.n_dist ? (uint32_t)(w.cav.dense.size() / w.cav.n_dist) : 0u;
       cl = !w.cav_lazy && ds.n_cav <= kLjCavInst && w.cav.dense.size() <= kLjCavDense && w.cav.n_ctx <= kLjCavCtx &&
@@ -2337,13 +2347,30 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.coherent = coherent;
       w.b_seq = j.seq;
     }
-    static const char* const lj_names[4] = {"void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)",
+    static const char* const lj_names[8] = {"void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)",
                                             "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)",
                                             "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)",
-                                            "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)"};
-    const int v = (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
-    if (cl || !aql_try(lj_names[v], &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves)))
+                                            "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)",
+                                            "void gck::k_label_join<24, 16u, 32u, true>(gck::LjArgs)",
+                                            "void gck::k_label_join<24, 32u, 32u, true>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 16u, 32u, true>(gck::LjArgs)",
+                                            "void gck::k_label_join<32, 32u, 32u, true>(gck::LjArgs)"};
+    const int v = (cl ? 4 : 0) + (ds.lj_bits == 24 ? 0 : 2) + (ds.lj_sw == 16 ? 0 : 1);
+    const AqlKernel* ak = aql_ok ? aql_kernel(e.aql, lj_names[v]) : nullptr;
+    if (cav && ak) {
+      j.cx = static_cast<const Ctx*>(aql_extra(w));  // (written with the arguments)
+    } else if (cav) {
+      *w.h_ctx = c;
+      HIP_OK(hipMemcpyAsync(w.d_ctx, w.h_ctx, sizeof(Ctx), hipMemcpyHostToDevice, st));
+      j.cx = w.d_ctx;
+    }
+    if (ak) {
+      aql_dispatch(*e.aql, w, *ak, &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves), w.b_timed,
+                   cav ? &c : nullptr, cav ? sizeof(Ctx) : 0);
+      w.b_aql = true;
+    } else {
       lj_launch(ds, j, n, st, w.b_timed ? w.ev0 : nullptr, w.b_timed && !w.b_chained ? w.ev1 : nullptr, cl);
+    }
   } else if (cj) {
     CjArgs j{};
     j.items = d_items;
@@ -2830,8 +2857,8 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
     w.b_xperm = pin_out ? perm : w.h_perm;
     w.b_xerr = pin_out ? err : w.h_err;
   }
-  if (w.cav_on) HIP_OK(hipMemsetAsync(w.cav_flag, 0, n, w.b_st));
   w.b_bundles = !(e.cfg.flags & GCK_FLAG_NO_BUNDLE);
+  if (w.cav_on && !w.b_bundles) HIP_OK(hipMemsetAsync(w.cav_flag, 0, n, w.b_st));  // (bundles_launch: its own)
   if (w.b_bundles) bundles_launch(e, w, w.b_items, n, now_us, w.b_dperm, w.b_derr, w.b_st, host);
   w.state = 1;
 }
@@ -2874,10 +2901,10 @@ static void caveat_passes(Engine& e, Workspace& w) {
         throw Error(GCK_E_DEVICE, "engine invariant violated: caveat pair request");
     }
     evaluate_pairs(e, w, keys);
-    upload_cav_map(w, st);
     HIP_OK(hipMemsetAsync(w.req_set, 0xFF, (size_t)kReqSet * 8, st));
     HIP_OK(hipMemsetAsync(w.req_cnt, 0, 4, st));
     HIP_OK(hipMemsetAsync(w.cav_flag, 0, w.b_n, st));
+    upload_cav_map(w, st);  // (ends with a synchronisation: the pass may be dispatched into an HSA queue)
     w.b_cav_req = w.b_cav_err = 0;
     if (w.b_bundles)
       bundles_launch(e, w, w.b_items, w.b_n, w.b_now, w.b_dperm, w.b_derr, st, w.b_hperm != nullptr);

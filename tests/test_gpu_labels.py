@@ -295,6 +295,56 @@ def test_caveat_plane(seed, lazy):
         assert st["caveat_passes"] >= 1, st
 
 
+@pytest.mark.parametrize("lazy", [False, True])
+def test_caveat_plane_on_the_engine_queue(lazy):
+    """Device batches with check contexts on the engine's stream: the label join with the caveat
+    plane is dispatched into the engine's HSA queue (aql.inc) — its Ctx written with the kernel
+    arguments, the checks' caveat flags cleared by the join itself — and later batches (chained
+    behind bundles) launch through HIP; a lazy batch's rerun passes follow it. Every batch
+    bit-exact against the oracle."""
+    import os
+
+    import numpy as np
+    import torch
+    rng = random.Random(5)
+    tuples, checks = _caveat_plane_graph(rng)
+    ctxs = [rng.choice(CAV_CONTEXTS) for _ in checks]
+    if lazy:
+        ctxs = [dict(c or {}, k=i) for i, c in enumerate(ctxs)]
+    ck = oracle_for(CAV_PLANE, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c), x)) for c, x in zip(checks, ctxs)]
+    e = E.Engine()
+    e.load_schema(CAV_PLANE)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    items = e.make_items([parse_check(c) for c in checks])
+    texts, slots = [], {}
+    for i, x in enumerate(ctxs):
+        if x is None:
+            continue
+        js = json.dumps(x, sort_keys=True)
+        if js not in slots:
+            texts.append(js)
+            slots[js] = len(texts)
+        items[i]["context_slot"] = slots[js]
+    n = len(items)
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).cuda()
+    e.reset_stats()
+    for rnd in range(4):
+        perm = torch.full((n,), 0xFF, dtype=torch.uint8, device="cuda")
+        err = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        e.submit(d_items.data_ptr(), n, perm.data_ptr(), err.data_ptr(), now_us=gen.NOW_US, contexts=texts,
+                 device=True, engine_stream=True).wait()
+        got = [(int(p), int(x)) for p, x in zip(perm.cpu().numpy(), err.cpu().numpy())]
+        bad = [(c, x, w, g) for c, x, w, g in zip(checks, ctxs, want, got) if w != g]
+        assert not bad, (rnd, bad[:10])
+    st = e.stats()
+    e.close()
+    assert st["label_checks"] >= 0.8 * 4 * n, st["label_checks"]
+    if os.path.exists(os.path.join(os.path.dirname(E.__file__), "libgck_kernels.co")):
+        assert st["aql_batches"] >= 1, st
+
+
 def test_caveat_plane_without_contexts():
     """No check contexts: a subject reached only through partial caveats is CONDITIONAL; one
     decided by its stored context alone is a plain grant or none."""
