@@ -616,7 +616,8 @@ def main():
         torch.cuda.synchronize()
         st_solo = eng.stats()
         eng.set_profile(False)
-        progress("solo launches done")
+        progress(f"solo launches done: {int(st_solo['bundle_launches'])} timed, {st_solo['bundle_ms']:.3f} ms, "
+                 f"{int(st_solo['aql_batches'])} dispatched into the engine's queues")
     if args.partitioned and not args.no_profile:
         # the partitioned join's own kernels timed by their events (k_label_join on one rank;
         # k_pj_pack + k_pj_decide on several, the exchange between them not included), the

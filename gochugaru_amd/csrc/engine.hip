@@ -2300,7 +2300,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // kernarg block and which clears the checks' caveat flags itself — nothing on the HIP stream)
   const bool aql_ok = w.b_own_stream && !host_out && !w.b_chained && ctr_was_clean && e.aql &&
                       w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
-                      (aql_timed || !w.b_timed);
+                      ((aql_timed && e.aql->tick_hz) || !w.b_timed);
   w.b_aql = false;
   const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok);
   const uint32_t coherent = 0u;  // (results are published by the kernel end's write-back)
