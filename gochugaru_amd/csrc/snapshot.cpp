@@ -7,6 +7,11 @@
 // expiry times), sorts every row ascending (wildcard id 0xFFFFFFFF sorts last) and keeps the
 // last write of a duplicate relationship (TOUCH semantics).
 #include <algorithm>
+#include <exception>
+#include <chrono>
+#include <mutex>
+#include <functional>
+#include <condition_variable>
 #include <atomic>
 #include <cstring>
 #include <numeric>
@@ -337,6 +342,81 @@ void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck
 // counting pass into the groups (a batch touches a few kinds), then per group a stable LSD radix
 // sort of the 64-bit (object << 32 | subject) keys in 11-bit digits, digits constant over the
 // group skipped (a comparison sort of a 10K-update batch cost ~0.2 ms of the Watch step).
+// A few resident workers for the per-group work of a Watch batch: starting threads per batch would
+// cost more than the work (a config-5 batch sorts 4 groups of ~2.5 K keys, ~15 us each). Workers
+// spin briefly after a job (Watch batches of a stream arrive every few hundred microseconds), then
+// sleep. One pool per engine, joined when the engine goes.
+struct GroupPool {
+  struct Run {  // one call's work: a worker that wakes late only ever finds it exhausted
+    const std::function<void(size_t)>* job;
+    size_t n;
+    std::atomic<size_t> next{0}, done{0};
+  };
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::shared_ptr<Run> cur;
+  uint64_t gen = 0;
+  bool stop = false;
+  std::atomic<uint64_t> gen_a{0};
+
+  explicit GroupPool(unsigned workers) {
+    for (unsigned k = 0; k < workers; ++k) th.emplace_back([this] { loop(); });
+  }
+  ~GroupPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+      ++gen;
+      gen_a.store(gen);
+    }
+    cv.notify_all();
+    for (std::thread& t : th) t.join();
+  }
+  static void work(Run& r) {
+    for (size_t i; (i = r.next.fetch_add(1)) < r.n;) {
+      (*r.job)(i);
+      r.done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      // spin ~200 us for the next batch, then sleep
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_a.load(std::memory_order_acquire) == seen &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+        __builtin_ia32_pause();
+      std::shared_ptr<Run> r;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return gen != seen; });
+        seen = gen;
+        if (stop) return;
+        r = cur;
+      }
+      if (r) work(*r);
+    }
+  }
+  // f(i) for every i < count, the caller taking part; returns when all are done
+  void run(size_t count, const std::function<void(size_t)>& f) {
+    auto r = std::make_shared<Run>();
+    r->job = &f;
+    r->n = count;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      cur = r;
+      ++gen;
+      gen_a.store(gen, std::memory_order_release);
+    }
+    cv.notify_all();
+    work(*r);
+    while (r->done.load(std::memory_order_acquire) < count) __builtin_ia32_pause();
+    std::lock_guard<std::mutex> lk(mu);
+    if (cur == r) cur.reset();
+  }
+};
+
 std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n) {
   PhaseClock pc("group");
   const Schema& sc = *e.schema;
@@ -406,8 +486,9 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
   }
   pc.mark("scatter");
   std::vector<UpdateGroup> out(G);
-  std::vector<uint32_t> cnt;
-  for (size_t gi = 0; gi < G; ++gi) {
+  // one group (disjoint ranges of a, b and out: the groups run in parallel)
+  auto sort_group = [&](size_t gi) {
+    std::vector<uint32_t> cnt;
     const size_t lo = start[gi], hi = start[gi + 1];
     // stable sort by key (a later write of a key stays after the earlier ones): one counting pass
     // on the key's top bits into ~one bucket per update, then an insertion sort of each bucket
@@ -478,6 +559,23 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
     g.is_ext.resize(w);
     g.cav.resize(w);
     g.exp_us.resize(w);
+  };
+  if (G > 1 && n >= 4096) {  // (a small batch: the workers' wake-up would cost more than its sorts)
+    if (!e.group_pool) e.group_pool = std::make_shared<GroupPool>(3u);
+    std::exception_ptr failed;
+    std::mutex fail_mu;
+    const std::function<void(size_t)> f = [&](size_t gi) {
+      try {
+        sort_group(gi);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(fail_mu);
+        if (!failed) failed = std::current_exception();
+      }
+    };
+    e.group_pool->run(G, f);
+    if (failed) std::rethrow_exception(failed);
+  } else {
+    for (size_t gi = 0; gi < G; ++gi) sort_group(gi);
   }
   pc.mark("sort");
   return out;

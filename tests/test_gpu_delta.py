@@ -238,5 +238,13 @@ def test_skewed_batch_on_one_object():
         probe = checks + [f"group:g{rnd}#member@user:u{k}" for k in range(200)] + \
             [f"group:g{rnd + 10}#member@user:u{k}" for k in range(200)]
         assert engine_results(e, probe) == oracle_results(schema, store, probe), rnd
+    # a batch large enough for the grouping's resident workers (>= 4096 updates, several groups)
+    ups = [(rng.choice(["CREATE", "DELETE", "TOUCH"]), f"group:g{rng.randrange(120)}#member@user:u{rng.randrange(200)}")
+           for _ in range(5000)]
+    ups += [(rng.choice(["CREATE", "DELETE"]), f"doc:d{rng.randrange(80)}#viewer@group:g{rng.randrange(30)}#member")
+            for _ in range(600)]
+    e.apply_updates_text(9, "\n".join(f"{op} {line}" for op, line in ups))
+    apply_to_store(store, ups)
+    assert engine_results(e, checks) == oracle_results(schema, store, checks)
     assert e.tuple_count == len(store)
     e.close()
