@@ -274,6 +274,8 @@ struct Workspace {
   size_t cav_dyn_cap = 0;
   uint32_t* cav_slot = nullptr;  // dense: each slot's distinct context (CavCall::of_slot)
   size_t cav_slot_cap = 0;
+  std::vector<uint8_t> cav_dyn_up;    // what cav_dyn / cav_slot hold (a call with the same table
+  std::vector<uint32_t> cav_slot_up;  // as the workspace's previous one uploads nothing)
   unsigned long long* cav_keys = nullptr;
   uint8_t* cav_vals = nullptr;
   size_t cav_map_cap = 0;       // slots of the device map (a power of two)
@@ -2702,12 +2704,17 @@ static void stage_caveats(Workspace& w, CavCall&& call, hipStream_t st) {
   w.cav_parsed.clear();
   if (!w.cav_on) return;
   if (!w.cav_lazy) {
+    if (w.cav.dense == w.cav_dyn_up && w.cav.of_slot == w.cav_slot_up) return;  // (on the device already)
+    w.cav_dyn_up.clear();
+    w.cav_slot_up.clear();
     grow(w, w.cav_dyn, w.cav_dyn_cap, w.cav.dense.size());
     grow(w, w.cav_slot, w.cav_slot_cap, w.cav.of_slot.size());
     // pageable sources: complete when the calls return
     HIP_OK(hipMemcpyAsync(w.cav_dyn, w.cav.dense.data(), w.cav.dense.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(w.cav_slot, w.cav.of_slot.data(), w.cav.of_slot.size() * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipStreamSynchronize(st));
+    w.cav_dyn_up = w.cav.dense;
+    w.cav_slot_up = w.cav.of_slot;
     return;
   }
   if (!w.req_set) {
