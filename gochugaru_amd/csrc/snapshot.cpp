@@ -470,26 +470,27 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
   std::sort(by_kind.begin(), by_kind.end(), [&](uint32_t x, uint32_t y) { return kinds[x] < kinds[y]; });
   for (size_t j = 0; j < G; ++j) rank[by_kind[j]] = (uint32_t)j;
   std::vector<size_t> start(G + 1, 0);
-  for (size_t i = 0; i < n; ++i) ++start[rank[g_of[i]] + 1];
-  for (size_t j = 0; j < G; ++j) start[j + 1] += start[j];
-  {
-    std::vector<size_t> at(start.begin(), start.end() - 1);
-    // the sort records carry what the groups need (upsert, expiration present, caveat) next to
-    // the update's index, so that only updates with an expiration are read again
-    for (size_t i = 0; i < n; ++i) {
-      const gck_tuple& t = ups[i].tuple;
-      const uint64_t up = ups[i].op != GCK_UPDATE_DELETE ? 1 : 0;
-      a[at[rank[g_of[i]]]++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
-                                ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) |
-                                    t.caveat};
-    }
+  for (size_t i = 0; i < n; ++i) {
+    g_of[i] = rank[g_of[i]];
+    ++start[g_of[i] + 1];
   }
-  pc.mark("scatter");
+  for (size_t j = 0; j < G; ++j) start[j + 1] += start[j];
+  pc.mark("count");
   std::vector<UpdateGroup> out(G);
-  // one group (disjoint ranges of a, b and out: the groups run in parallel)
+  // one group (disjoint ranges of a, b and out: the groups run in parallel; each gathers its own
+  // updates, so that no core writes lines another core's group just read)
   auto sort_group = [&](size_t gi) {
     std::vector<uint32_t> cnt;
     const size_t lo = start[gi], hi = start[gi + 1];
+    // the sort records carry what the group needs (upsert, expiration present, caveat) next to
+    // the update's index, so that only updates with an expiration are read again
+    for (size_t i = 0, at = lo; i < n && at < hi; ++i) {
+      if (g_of[i] != gi) continue;
+      const gck_tuple& t = ups[i].tuple;
+      const uint64_t up = ups[i].op != GCK_UPDATE_DELETE ? 1 : 0;
+      a[at++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
+                 ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) | t.caveat};
+    }
     // stable sort by key (a later write of a key stays after the earlier ones): one counting pass
     // on the key's top bits into ~one bucket per update, then an insertion sort of each bucket
     // (a bucket that a skewed batch fills — many subjects of one object — is merge-sorted)
