@@ -56,7 +56,7 @@ def parse():
                     help="engine without the label-join stage (GCK_FLAG_NO_LABELS): the A/B of the join")
     ap.add_argument("--cpu-max-batches", type=int, default=400)
     ap.add_argument("--no-oracle", action="store_true", help="skip the host oracle (no roofline, no CPU baseline)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "aql_pmc", "traffic.json"),
+    ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC HBM bytes per batch (tools/gpu.sh profile, calibrated by tools/gather_probe)")
     ap.add_argument("--host-steps", type=int, default=200, help="PCIe-inclusive host-buffer steps (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None,
@@ -817,7 +817,12 @@ def main():
         ms = ms_a + ms_b
         achieved = b_alg / (ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
-        if args.traffic_json and os.path.exists(args.traffic_json) and WL.kind == "nested":
+        # (the counter passes of this workload's own batches, tools/gpu.sh profile)
+        if args.traffic_json is None:
+            args.traffic_json = os.path.join(ROOT, "profiles", "r04", {"nested": "aql_pmc", "gdocs": "pmc_gdocs",
+                                                                        "github": "pmc_github"}.get(WL.kind, "-"),
+                                             "traffic.json")
+        if args.traffic_json and os.path.exists(args.traffic_json) and WL.kind in ("nested", "gdocs", "github"):
             tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_batch")
             traffic_src = os.path.relpath(args.traffic_json, os.path.dirname(os.path.abspath(__file__)))
