@@ -7,6 +7,7 @@
 // expiry times), sorts every row ascending (wildcard id 0xFFFFFFFF sorts last) and keeps the
 // last write of a duplicate relationship (TOUCH semantics).
 #include <algorithm>
+#include <unistd.h>
 #include <exception>
 #include <chrono>
 #include <mutex>
@@ -360,10 +361,16 @@ struct GroupPool {
   bool stop = false;
   std::atomic<uint64_t> gen_a{0};
 
+  const pid_t owner = getpid();  // (a forked child has the object but not the threads)
+
   explicit GroupPool(unsigned workers) {
     for (unsigned k = 0; k < workers; ++k) th.emplace_back([this] { loop(); });
   }
   ~GroupPool() {
+    if (getpid() != owner) {  // nothing to join here: the workers live in the parent (their handles
+      (void)new std::vector<std::thread>(std::move(th));  // are kept, never joined nor destroyed)
+      return;
+    }
     {
       std::lock_guard<std::mutex> lk(mu);
       stop = true;
