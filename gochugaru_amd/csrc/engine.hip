@@ -1361,6 +1361,9 @@ int device_init(Engine& e) {
   hipStream_t fs = nullptr;
   HIP_OK(hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
   e.free_stream = fs;
+  hipEvent_t dev = nullptr;
+  HIP_OK(hipEventCreateWithFlags(&dev, hipEventDisableTiming));
+  e.delta_ev = dev;
   e.device_ready = true;
   return 0;
 }
@@ -1457,6 +1460,8 @@ void device_free(Engine& e) {
     (void)hipStreamSynchronize((hipStream_t)e.free_stream);
     (void)hipStreamDestroy((hipStream_t)e.free_stream);
     e.free_stream = nullptr;
+    if (e.delta_ev) (void)hipEventDestroy((hipEvent_t)e.delta_ev);
+    e.delta_ev = nullptr;
     e.device_ready = false;
   }
 }

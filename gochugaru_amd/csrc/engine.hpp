@@ -200,6 +200,7 @@ struct Engine {
   uint64_t generation = 0;        // bumped by every device snapshot (commit, Watch batch)
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
+  void* delta_ev = nullptr;       // hipEvent_t: a Watch batch's merge totals are back (delta.inc)
   size_t delta_scratch_cap = 0;
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
