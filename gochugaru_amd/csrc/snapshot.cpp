@@ -345,8 +345,7 @@ void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck
 // group skipped (a comparison sort of a 10K-update batch cost ~0.2 ms of the Watch step).
 // A few resident workers for the per-group work of a Watch batch: starting threads per batch would
 // cost more than the work (a config-5 batch sorts 4 groups of ~2.5 K keys, ~15 us each). Workers
-// spin briefly after a job (Watch batches of a stream arrive every few hundred microseconds), then
-// sleep. One pool per engine, joined when the engine goes.
+// sleep between batches. One pool per engine, joined when the engine goes.
 struct GroupPool {
   struct Run {  // one call's work: a worker that wakes late only ever finds it exhausted
     const std::function<void(size_t)>* job;
@@ -359,7 +358,6 @@ struct GroupPool {
   std::shared_ptr<Run> cur;
   uint64_t gen = 0;
   bool stop = false;
-  std::atomic<uint64_t> gen_a{0};
 
   const pid_t owner = getpid();  // (a forked child has the object but not the threads)
 
@@ -375,7 +373,6 @@ struct GroupPool {
       std::lock_guard<std::mutex> lk(mu);
       stop = true;
       ++gen;
-      gen_a.store(gen);
     }
     cv.notify_all();
     for (std::thread& t : th) t.join();
@@ -389,11 +386,8 @@ struct GroupPool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      // spin ~200 us for the next batch, then sleep
-      const auto t0 = std::chrono::steady_clock::now();
-      while (gen_a.load(std::memory_order_acquire) == seen &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
-        __builtin_ia32_pause();
+      // (no spinning between batches: a spinning worker slowed the caller's own host phases —
+      // validation 22 -> 50-80 us on config 5 — more than its wake-up costs)
       std::shared_ptr<Run> r;
       {
         std::unique_lock<std::mutex> lk(mu);
@@ -414,7 +408,6 @@ struct GroupPool {
       std::lock_guard<std::mutex> lk(mu);
       cur = r;
       ++gen;
-      gen_a.store(gen, std::memory_order_release);
     }
     cv.notify_all();
     work(*r);
