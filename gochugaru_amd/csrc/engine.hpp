@@ -205,7 +205,6 @@ struct Engine {
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
   std::vector<uint64_t> group_scratch;  // group_updates' sort buffers, kept across Watch batches
-  std::shared_ptr<struct GroupPool> group_pool;  // snapshot.cpp: resident workers for the per-group sorts
   // merged-CSR arrays of retired snapshots kept for the next Watch batch's merge (engine.hip
   // ralloc / retire_array): bytes -> array, and every array ralloc handed out -> its bytes
   std::multimap<size_t, void*> recycle;

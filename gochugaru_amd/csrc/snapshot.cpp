@@ -7,12 +7,6 @@
 // expiry times), sorts every row ascending (wildcard id 0xFFFFFFFF sorts last) and keeps the
 // last write of a duplicate relationship (TOUCH semantics).
 #include <algorithm>
-#include <unistd.h>
-#include <exception>
-#include <chrono>
-#include <mutex>
-#include <functional>
-#include <condition_variable>
 #include <atomic>
 #include <cstring>
 #include <numeric>
@@ -343,80 +337,6 @@ void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck
 // counting pass into the groups (a batch touches a few kinds), then per group a stable LSD radix
 // sort of the 64-bit (object << 32 | subject) keys in 11-bit digits, digits constant over the
 // group skipped (a comparison sort of a 10K-update batch cost ~0.2 ms of the Watch step).
-// A few resident workers for the per-group work of a Watch batch: starting threads per batch would
-// cost more than the work (a config-5 batch sorts 4 groups of ~2.5 K keys, ~15 us each). Workers
-// sleep between batches. One pool per engine, joined when the engine goes.
-struct GroupPool {
-  struct Run {  // one call's work: a worker that wakes late only ever finds it exhausted
-    const std::function<void(size_t)>* job;
-    size_t n;
-    std::atomic<size_t> next{0}, done{0};
-  };
-  std::vector<std::thread> th;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::shared_ptr<Run> cur;
-  uint64_t gen = 0;
-  bool stop = false;
-
-  const pid_t owner = getpid();  // (a forked child has the object but not the threads)
-
-  explicit GroupPool(unsigned workers) {
-    for (unsigned k = 0; k < workers; ++k) th.emplace_back([this] { loop(); });
-  }
-  ~GroupPool() {
-    if (getpid() != owner) {  // nothing to join here: the workers live in the parent (their handles
-      (void)new std::vector<std::thread>(std::move(th));  // are kept, never joined nor destroyed)
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      stop = true;
-      ++gen;
-    }
-    cv.notify_all();
-    for (std::thread& t : th) t.join();
-  }
-  static void work(Run& r) {
-    for (size_t i; (i = r.next.fetch_add(1)) < r.n;) {
-      (*r.job)(i);
-      r.done.fetch_add(1, std::memory_order_release);
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      // (no spinning between batches: a spinning worker slowed the caller's own host phases —
-      // validation 22 -> 50-80 us on config 5 — more than its wake-up costs)
-      std::shared_ptr<Run> r;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return gen != seen; });
-        seen = gen;
-        if (stop) return;
-        r = cur;
-      }
-      if (r) work(*r);
-    }
-  }
-  // f(i) for every i < count, the caller taking part; returns when all are done
-  void run(size_t count, const std::function<void(size_t)>& f) {
-    auto r = std::make_shared<Run>();
-    r->job = &f;
-    r->n = count;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      cur = r;
-      ++gen;
-    }
-    cv.notify_all();
-    work(*r);
-    while (r->done.load(std::memory_order_acquire) < count) __builtin_ia32_pause();
-    std::lock_guard<std::mutex> lk(mu);
-    if (cur == r) cur.reset();
-  }
-};
-
 std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n) {
   PhaseClock pc("group");
   const Schema& sc = *e.schema;
@@ -470,27 +390,25 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
   std::sort(by_kind.begin(), by_kind.end(), [&](uint32_t x, uint32_t y) { return kinds[x] < kinds[y]; });
   for (size_t j = 0; j < G; ++j) rank[by_kind[j]] = (uint32_t)j;
   std::vector<size_t> start(G + 1, 0);
-  for (size_t i = 0; i < n; ++i) {
-    g_of[i] = rank[g_of[i]];
-    ++start[g_of[i] + 1];
-  }
+  for (size_t i = 0; i < n; ++i) ++start[rank[g_of[i]] + 1];
   for (size_t j = 0; j < G; ++j) start[j + 1] += start[j];
-  pc.mark("count");
-  std::vector<UpdateGroup> out(G);
-  // one group (disjoint ranges of a, b and out: the groups run in parallel; each gathers its own
-  // updates, so that no core writes lines another core's group just read)
-  auto sort_group = [&](size_t gi) {
-    std::vector<uint32_t> cnt;
-    const size_t lo = start[gi], hi = start[gi + 1];
-    // the sort records carry what the group needs (upsert, expiration present, caveat) next to
+  {
+    std::vector<size_t> at(start.begin(), start.end() - 1);
+    // the sort records carry what the groups need (upsert, expiration present, caveat) next to
     // the update's index, so that only updates with an expiration are read again
-    for (size_t i = 0, at = lo; i < n && at < hi; ++i) {
-      if (g_of[i] != gi) continue;
+    for (size_t i = 0; i < n; ++i) {
       const gck_tuple& t = ups[i].tuple;
       const uint64_t up = ups[i].op != GCK_UPDATE_DELETE ? 1 : 0;
-      a[at++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
-                 ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) | t.caveat};
+      a[at[rank[g_of[i]]]++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
+                                ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) |
+                                    t.caveat};
     }
+  }
+  pc.mark("scatter");
+  std::vector<UpdateGroup> out(G);
+  std::vector<uint32_t> cnt;
+  for (size_t gi = 0; gi < G; ++gi) {
+    const size_t lo = start[gi], hi = start[gi + 1];
     // stable sort by key (a later write of a key stays after the earlier ones): one counting pass
     // on the key's top bits into ~one bucket per update, then an insertion sort of each bucket
     // (a bucket that a skewed batch fills — many subjects of one object — is merge-sorted)
@@ -560,23 +478,6 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
     g.is_ext.resize(w);
     g.cav.resize(w);
     g.exp_us.resize(w);
-  };
-  if (G > 1 && n >= 4096) {  // (a small batch: the workers' wake-up would cost more than its sorts)
-    if (!e.group_pool) e.group_pool = std::make_shared<GroupPool>(3u);
-    std::exception_ptr failed;
-    std::mutex fail_mu;
-    const std::function<void(size_t)> f = [&](size_t gi) {
-      try {
-        sort_group(gi);
-      } catch (...) {
-        std::lock_guard<std::mutex> lk(fail_mu);
-        if (!failed) failed = std::current_exception();
-      }
-    };
-    e.group_pool->run(G, f);
-    if (failed) std::rethrow_exception(failed);
-  } else {
-    for (size_t gi = 0; gi < G; ++gi) sort_group(gi);
   }
   pc.mark("sort");
   return out;
