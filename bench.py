@@ -4,23 +4,26 @@ Workload (BASELINE.json metric "permission checks/sec (whole node) at batch 64K,
 HBM GB/s vs peak"; config 4 of BASELINE.json configs, replicated-graph mode, which fits one
 MI355X): tests/synth.py builds the seeded graph on every rank (identical, replicated), the
 engine ingests it through the C ABI (gck_load_csr), and each step is one 65,536-item
-``doc#view@user`` batch per GPU with the items already resident in HBM: 2,000 distinct
-pre-generated batches, 8 in flight (gck_check_submit / gck_check_wait on the engine's own
-streams, driven by the compiled loop of libgck_driver.so). With N ranks every 64K request is cut
-into N contiguous slices, rank r checking slice r against its replica (no collective on the data
+``doc#view@user`` request per GPU as BASELINE.md:40-41 / SURVEY §8(d) define the step: the items
+start in host memory (pinned, gck_host_alloc: where a cgo caller builds its requests), cross to
+the GPU, are checked, and the results end in host memory — items H2D + kernels + results D2H
+inside the timed region. 2,000 distinct pre-generated requests, 8 in flight (gck_check_submit /
+gck_check_wait, the compiled loop of libgck_driver.so). With N ranks every 64K request is cut into
+N contiguous slices, rank r checking slice r against its replica (no collective on the data
 path): the node figure at batch 64K, strong scaling, value = (checks of the requests) /
 (max-over-ranks time); `weak_scaling` times every rank on its own 64K requests beside it.
-`baseline_step` is BASELINE.md:40-41's own step (one batch alone, H2D + kernels + D2H, median over
->= 20 batches after 3 warm-up ones). Configs 2, 3 run the same way; 5 (``--config mixed``) checks
-a batch per rank and step.
+`baseline_step` is BASELINE.md:40-41's lone-batch figure (one batch alone, median over >= 20
+batches after 3 warm-up ones); `device_resident` the same requests with the items already in HBM
+(the kernels' own throughput, never `value`). Configs 2, 3 run the same way; 5
+(``--config mixed``) checks a device-resident batch per rank and step beside its Watch batch.
 
 Also printed: the roofline of the dominant kernel (SURVEY.md §8d algorithmic bytes of a batch,
-counted by the oracle's counting mode, / the mean k_closure_join launch time from the kernel's
-own HIP events, batches one at a time after the timed region; `traffic` = HBM bytes per batch
-from rocprofv3 PMC, tools/gpu.sh profile -> profiles/r03/final/traffic.json), the PCIe-inclusive rate over
-host buffers (never `value`), and a CPU baseline: the C restatement oracle (16 host threads) on a
-bounded sample of the same batches, ~15 s of CPU work, with every sampled check compared against
-the GPU's answer (`oracle_agreement`).
+counted by the oracle's counting mode, / the mean stage-A launch time of device-resident batches
+one at a time after the timed region, from the queue's dispatch timestamps; `traffic` = HBM bytes
+per batch from rocprofv3 PMC), the host link's share (`pcie`), the process's placement on the
+GPU's NUMA node (`host_placement`), and a CPU baseline: the C restatement oracle (16 host
+threads) on a bounded sample of the same batches, ~15 s of CPU work, with every sampled check
+compared against the GPU's answer (`oracle_agreement`).
 """
 import argparse
 import collections
@@ -349,6 +352,9 @@ def main():
         init_group(args.part_backend if args.partitioned else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # the submitting thread (and so the writer of each request's items) on the GPU's NUMA node
+    from gochugaru_amd.engine import pin_to_device_node
+    placement = pin_to_device_node(local)
 
     from gochugaru_amd.engine import Engine, ITEM_DTYPE
 
@@ -484,6 +490,16 @@ def main():
         outs = [(torch.zeros(n_slice, dtype=torch.uint8, device=dev),
                  torch.zeros(n_slice, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
         streams = [torch.cuda.Stream(dev) for _ in range(depth)]
+        # `value`'s path (BASELINE.md:40-41, SURVEY §8d: items H2D + kernels + results D2H): the
+        # same requests in host memory — pinned, from gck_host_alloc, where a cgo caller builds its
+        # requests — and the results back into host memory. One allocation per array, every
+        # batch its own slice (no step re-reads a batch another step read).
+        h_items = eng.host_array(n_rot * n_slice, ITEM_DTYPE)
+        h_perm = eng.host_array(n_rot * n_slice, np.uint8)
+        h_err = eng.host_array(n_rot * n_slice, np.int32)
+        for k in range(n_rot):
+            h_items[k * n_slice:(k + 1) * n_slice] = rot[k].cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+        h_ptr = lambda a, k: a.ctypes.data + k * n_slice * a.itemsize
         torch.cuda.synchronize()
         cursor = {"k": 0}
         pending = collections.deque()
@@ -493,9 +509,8 @@ def main():
             cursor["k"] += 1
             if len(pending) >= depth:
                 pending.popleft().wait()
-            pending.append(eng.submit(rot[k].data_ptr(), n_slice, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
-                                      device=True, stream=streams[k % depth].cuda_stream,
-                                      engine_stream=bool(args.engine_streams)))
+            sl = slice(k * n_slice, (k + 1) * n_slice)
+            pending.append(eng.submit_into(h_items[sl], h_perm[sl], h_err[sl]))
 
         def drain():
             while pending:
@@ -512,9 +527,8 @@ def main():
                 k0 = cursor["k"] + sum(c for c, _ in prepared.values())
                 ks = range(k0, k0 + count)
                 prepared[len(prepared)] = (count, eng.prepare_batches(
-                    [rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
-                    [outs[k][1].data_ptr() for k in ks], n_slice, depth,
-                    [streams[(k - k0) % depth].cuda_stream for k in ks], engine_streams=bool(args.engine_streams)))
+                    [h_ptr(h_items, k) for k in ks], [h_ptr(h_perm, k) for k in ks], [h_ptr(h_err, k) for k in ks],
+                    n_slice, depth, host=True))
 
             def run_steps(count):
                 c, run = prepared.pop(min(prepared))
@@ -564,18 +578,54 @@ def main():
         _driver().gckd_set_trace(None, 0)
     progress(f"timed region: {args.steps} steps in {elapsed * 1e3:.2f} ms"
              + (f" (compiled loop {loop_s['s'] * 1e3:.3f} ms)" if native else ""))
-    # weak scaling beside the node figure (N > 1): every rank checks its own whole requests
-    weak = None
-    if native and world > 1 and WL.kind in ("nested", "gdocs", "github") and not args.partitioned:
-        n_w = min(args.steps, 500)
-        n_wr = n_w + 2 * depth
-        w_rot = [WL.checks(args.batch, 700000 + 100003 * rank + k) for k in range(n_wr)]
-        w_out = [(torch.zeros(args.batch, dtype=torch.uint8, device=dev),
-                  torch.zeros(args.batch, dtype=torch.int32, device=dev)) for _ in range(n_wr)]
-        mkw = lambda ks: eng.prepare_batches([w_rot[k].data_ptr() for k in ks], [w_out[k][0].data_ptr() for k in ks],
-                                             [w_out[k][1].data_ptr() for k in ks], args.batch, depth,
+    pipelined = native and WL.kind in ("nested", "gdocs", "github") and not args.partitioned
+    # the same requests device-resident (items already in HBM, results left there; never `value`):
+    # what the engine sustains without the PCIe transfers, the kernels' own throughput. The timed
+    # batches again, after warm-up batches of their own, on the engine's streams.
+    device_resident = None
+    if pipelined:
+        mkd = lambda ks: eng.prepare_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
+                                             [outs[k][1].data_ptr() for k in ks], n_slice, depth,
                                              [streams[j % depth].cuda_stream for j in range(len(ks))],
                                              engine_streams=bool(args.engine_streams))
+        d_warm, d_run = mkd(range(args.warm)), mkd(range(args.warm, args.warm + args.steps))
+        torch.cuda.synchronize()
+        d_warm.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        td = time.perf_counter()
+        d_loop = d_run.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        td = time.perf_counter() - td
+        if world > 1:
+            tt = torch.tensor([td], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            td = float(tt[0])
+        device_resident = {"value": round(args.batch * args.steps / td, 1), "unit": "checks/s", "seconds": td,
+                           "ms_per_step": round(td / args.steps * 1e3, 4), "compiled_loop_ms": round(d_loop * 1e3, 4),
+                           "inflight": depth, "steps": args.steps,
+                           "note": "the same rotated requests with the items already in HBM and the results left "
+                                   "there (no PCIe in the step): the kernels' own throughput, not `value`"}
+        progress(f"device-resident phase: {td * 1e3:.2f} ms")
+    # weak scaling beside the node figure (N > 1): every rank checks its own whole requests (host
+    # buffers, as `value`)
+    weak = None
+    if pipelined and world > 1:
+        n_w = min(args.steps, 500)
+        n_wr = n_w + 2 * depth
+        w_items = eng.host_array(n_wr * args.batch, ITEM_DTYPE)
+        w_perm = eng.host_array(n_wr * args.batch, np.uint8)
+        w_err = eng.host_array(n_wr * args.batch, np.int32)
+        for k in range(n_wr):
+            w_items[k * args.batch:(k + 1) * args.batch] = (
+                WL.checks(args.batch, 700000 + 100003 * rank + k).cpu().numpy().view(ITEM_DTYPE).reshape(-1))
+        wp = lambda a, k: a.ctypes.data + k * args.batch * a.itemsize
+        mkw = lambda ks: eng.prepare_batches([wp(w_items, k) for k in ks], [wp(w_perm, k) for k in ks],
+                                             [wp(w_err, k) for k in ks], args.batch, depth, host=True)
         w_warm, w_run = mkw(range(2 * depth)), mkw(range(2 * depth, n_wr))
         torch.cuda.synchronize()
         w_warm.run()
@@ -593,19 +643,28 @@ def main():
         weak = {"value": round(world * args.batch * n_w / tw, 1), "unit": "checks/s", "steps": n_w,
                 "ms_per_step": round(tw / n_w * 1e3, 4), "scaling": "weak",
                 "note": f"every rank checks its own {args.batch}-check requests ({world} x {args.batch} checks per "
-                        f"step), max-over-ranks time"}
-        del w_rot, w_out
+                        f"step) from pinned host memory, results back to host memory, max-over-ranks time"}
+        del w_items, w_perm, w_err
         progress("weak-scaling phase done")
+    same_results = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned:  # the first timed batch and its results
-        items, (perm, err) = rot[args.warm], outs[args.warm]
+        items = rot[args.warm]
+        sl0 = slice(args.warm * n_slice, (args.warm + 1) * n_slice)
+        perm, err = torch.from_numpy(h_perm[sl0].copy()), torch.from_numpy(h_err[sl0].copy())
+        if device_resident is not None:  # every timed batch: host path == device-resident path
+            same_results = all(
+                (h_perm[k * n_slice:(k + 1) * n_slice] == outs[k][0].cpu().numpy()).all() and
+                (h_err[k * n_slice:(k + 1) * n_slice] == outs[k][1].cpu().numpy()).all()
+                for k in range(args.warm, args.warm + args.steps))
     if WL.kind == "quota":
         items, (perm, err) = q_rot[args.warm][0], q_out[args.warm]
     st = eng.stats()
     # per-launch time of the dominant kernel, alone on the GPU: the timed batches again, one at a
-    # time, stage A timed by its dispatch timestamps (the engine's HSA queues; HIP events for a
+    # time, device-resident (the kernel's own HBM roofline, without the PCIe reads of `value`'s
+    # path), stage A timed by its dispatch timestamps (the engine's HSA queues; HIP events for a
     # batch launched through HIP), every 4th batch of a workspace. With batches in flight a launch
     # also waits for the CUs the other batches hold, so the roofline uses these; `achieved_job` is
-    # the whole timed region.
+    # the whole device-resident phase.
     st_solo = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and not args.no_profile:
         eng.set_profile(True)  # the timed region ran without events (a timed launch holds back the others)
@@ -648,97 +707,83 @@ def main():
     res = perm.cpu().numpy()
     errs = err.cpu().numpy()
 
-    # ---- PCIe-inclusive rate (host buffers: H2D items + kernels + D2H results), never `value` --
-    # SURVEY §8(d)'s step: the items start in (pageable) host memory and the results end there;
-    # the same rotated batches, `depth` in flight (gck_check_submit with host buffers: each
-    # batch's copies overlap the other batches' kernels), and one at a time for reference.
+    # ---- the host-buffer path's other shapes (never `value`): one ctypes call per submit / wait,
+    # pageable numpy buffers through the engine's pinned staging, one batch at a time, and
+    # BASELINE.md:40-41's lone-batch median — over the first rotated batches, cycled
     host_rate = None
     baseline_step = None
     if WL.kind not in ("mixed", "quota") and not args.partitioned and args.host_steps > 0:
-        # (up to 32 of the rotated batches, cycled: pinned host memory per batch is 1.6 MB)
-        n_h = min(len(rot), max(32, args.warm + 1))
-        h_rot = [b.cpu().numpy().view(ITEM_DTYPE).reshape(-1).copy() for b in rot[:n_h]]
-        ref0 = (outs[args.warm][0].cpu().numpy(), outs[args.warm][1].cpu().numpy())
-        # the same batches in pinned host memory (gck_host_alloc: DMA straight from / into them)
-        p_rot = []
-        for b in h_rot:
-            a = eng.host_array(len(b), ITEM_DTYPE)
-            a[:] = b
-            p_rot.append((a, eng.host_array(len(b), np.uint8), eng.host_array(len(b), np.int32)))
+        n_h = min(len(rot), 32)
+        p_rot = [(h_items[k * n_slice:(k + 1) * n_slice], h_perm[k * n_slice:(k + 1) * n_slice].copy(),
+                  h_err[k * n_slice:(k + 1) * n_slice].copy()) for k in range(n_h)]
+        p_rot = [(a, eng.host_array(n_slice, np.uint8), eng.host_array(n_slice, np.int32)) for a, _, _ in p_rot]
+        h_rot = [a.copy() for a, _, _ in p_rot]  # pageable copies
+        ref0 = (h_perm[:n_slice].copy(), h_err[:n_slice].copy())  # batch 0 from the warm-up
 
         def host_run(n_batches, dq, pinned):
-            res, q = {}, collections.deque()
+            res_, q = {}, collections.deque()
             for j in range(n_batches):
-                k = j % len(h_rot)
+                k = j % n_h
                 if len(q) >= dq:
                     kk, b = q.popleft()
-                    res[kk] = b.wait()
+                    res_[kk] = b.wait()
                 q.append((k, eng.submit_into(*p_rot[k]) if pinned else eng.submit(h_rot[k])))
             while q:
                 kk, b = q.popleft()
-                res[kk] = b.wait()
-            return res
+                res_[kk] = b.wait()
+            return res_
 
         def timed(dq, pinned):
             host_run(args.warm, dq, pinned)
-            t0 = time.perf_counter()
+            t0_ = time.perf_counter()
             r = host_run(args.host_steps, dq, pinned)
-            dt = time.perf_counter() - t0
+            dt = time.perf_counter() - t0_
             return r, {"value": round(args.host_steps * n_slice / dt, 1),
                        "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
-
-        def timed_native(dq):
-            # the compiled loop (libgck_driver.so gckd_run_host) over the pinned batches, cycled
-            ks = [j % len(p_rot) for j in range(args.host_steps)]
-            wk = [j % len(p_rot) for j in range(args.warm)]
-            mk = lambda kk: eng.prepare_batches([p_rot[k][0].ctypes.data for k in kk], [p_rot[k][1].ctypes.data for k in kk],
-                                                [p_rot[k][2].ctypes.data for k in kk], n_slice, dq, host=True)
-            warm_run, run = mk(wk), mk(ks)
-            warm_run.run()
-            dt = run.run()
-            k0_ = ks[-1]
-            return {k0_: (p_rot[k0_][1].copy(), p_rot[k0_][2].copy())}, {
-                "value": round(args.host_steps * n_slice / dt, 1), "ms_per_step": round(dt / args.host_steps * 1e3, 4)}
-        nres, main = timed_native(depth)
         hres, py_pinned = timed(depth, True)
         pres, pageable = timed(depth, False)
         _, one = timed(1, True)
         # BASELINE.md:40-41's own definition: 3 warm-up batches, then >= 20 batches, each one alone
-        # (items H2D, kernels, results D2H on the batch's stream: the compiled loop over pinned
-        # buffers, 1 in flight), checks/s = checks per batch / the MEDIAN batch time
+        # (items H2D, kernels, results D2H: the compiled loop over pinned buffers, 1 in flight),
+        # checks/s = checks per batch / the MEDIAN batch time
         from gochugaru_amd.engine import _driver
         import ctypes
         nb_med = max(20, min(200, args.host_steps))
-        kb = [j % len(p_rot) for j in range(3 + nb_med)]
+        kb = [j % n_h for j in range(3 + nb_med)]
         med_run = eng.prepare_batches([p_rot[k][0].ctypes.data for k in kb], [p_rot[k][1].ctypes.data for k in kb],
                                       [p_rot[k][2].ctypes.data for k in kb], n_slice, 1, host=True)
         stamps = np.zeros(2 * len(kb), dtype=np.float64)
         _driver().gckd_set_trace(stamps.ctypes.data_as(ctypes.c_void_p), len(kb))
         med_run.run()
         _driver().gckd_set_trace(None, 0)
-        ends = stamps[1::2]
-        per_batch = (ends - np.concatenate([[0.0], ends[:-1]]))[3:]
+        subs, ends = stamps[0::2], stamps[1::2]
+        prev = np.concatenate([[0.0], ends[:-1]])
+        per_batch = (ends - prev)[3:]
         med_s = float(np.median(per_batch))
         baseline_step = {"value": round(n_slice / med_s, 1), "unit": "checks/s", "median_batch_ms": round(med_s * 1e3, 4),
                          "p90_batch_ms": round(float(np.percentile(per_batch, 90)) * 1e3, 4),
+                         "median_submit_ms": round(float(np.median((subs - prev)[3:])) * 1e3, 4),
                          "batches": int(len(per_batch)), "warmup_batches": 3, "checks_per_batch": n_slice,
                          "definition": "BASELINE.md:40-41: checks per batch / median batch time over >= 20 batches "
                                        "after 3 warm-up batches, each batch alone (1 in flight): items H2D + kernels + "
                                        "results D2H (pinned gck_host_alloc buffers, the compiled submit/wait loop)"}
-        k0 = args.warm % len(h_rot)
-        kn = (args.host_steps - 1) % len(p_rot)
-        refn = (outs[kn][0].cpu().numpy(), outs[kn][1].cpu().numpy())
-        same = all(k0 in r and (r[k0][0] == ref0[0]).all() and (r[k0][1] == ref0[1]).all() for r in (hres, pres))
-        same = same and all((nres[kn][j] == refn[j]).all() for j in (0, 1))
-        host_rate = {**main, "unit": "checks/s", "inflight": depth, "driver": "native",
-                     "python_pinned": py_pinned, "pageable": pageable, "one_at_a_time": one,
-                     "same_results": bool(same),
-                     "note": "SURVEY 8(d)'s step: items H2D, kernels, results D2H, rotated batches; the compiled "
-                             "submit/wait loop (libgck_driver.so gckd_run_host) over host buffers in pinned memory "
-                             "(gck_host_alloc: 20-B items DMA'd from them, 1+4 B results DMA'd into them); "
-                             "`python_pinned`: the same through one ctypes call per submit/wait; `pageable`: numpy "
-                             "buffers through the engine's pinned staging copies; `one_at_a_time`: 1 in flight"}
+        same = all(0 in r and (r[0][0] == ref0[0]).all() and (r[0][1] == ref0[1]).all() for r in (hres, pres))
+        host_rate = {"python_pinned": py_pinned, "pageable": pageable, "one_at_a_time": one, "inflight": depth,
+                     "same_results": bool(same), "batches_cycled": n_h,
+                     "note": "`value`'s path through other callers: one ctypes call per submit/wait over pinned "
+                             "buffers (`python_pinned`), pageable numpy buffers through the engine's pinned staging "
+                             "(`pageable`), 1 in flight (`one_at_a_time`)"}
 
+    # `value`'s path is bound by the host link: 20 B of items in and 5 B of results out per check
+    pcie = None
+    if WL.kind in ("nested", "gdocs", "github") and not args.partitioned:
+        per_rank = args.batch * args.steps / world  # checks over this rank's own link
+        h2d, d2h = per_rank * 20 / elapsed / 1e9, per_rank * 5 / elapsed / 1e9
+        pcie = {"bound": "pcie", "achieved": round(h2d, 2), "peak": 63.0, "unit": "GB/s", "frac": round(h2d / 63.0, 4),
+                "d2h_GBs": round(d2h, 2), "bytes_per_check": {"h2d": 20, "d2h": 5},
+                "note": "per GPU: the items' host-to-device bytes of the timed region (the binding direction) over "
+                        "its time; peak = PCIe Gen5 x16 spec per direction (MI355X_MICROARCH.md); tools/pcie_probe "
+                        "measures 40-41 GB/s for the GPU's zero-copy reads and the copy engines on this platform"}
     progress("host-buffer runs done")
     # ---- host-side checker: oracle over the same graph (rank 0) ------------------------------
     # host threads for the oracle: the CPUs this process may use (affinity mask, cgroup quota),
@@ -838,7 +883,8 @@ def main():
                 "alg_bytes_per_launch": int(b_alg),
                 # the whole job: algorithmic bytes of every timed batch / the timed region (launches
                 # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)
-                "achieved_job": round(b_alg * args.steps / elapsed / 1e9, 3),
+                "achieved_job": round(b_alg * args.steps / device_resident["seconds"] / 1e9, 3)
+                if device_resident else None,
                 "inflight": depth,
                 "driver": args.driver if run_steps is not None or args.driver == "python" else "python",
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or 4,
@@ -866,13 +912,15 @@ def main():
         extra = int(max(0, min(args.cpu_max_batches, args.cpu_seconds / max(per_batch, 1e-6))) - 1)
         # the timed batches with the results the timed region produced, then further batches
         timed = list(range(args.warm, args.warm + args.steps)) if WL.kind != "mixed" else []
-        batches = ([(rot[k], outs[k][0], outs[k][1]) for k in timed[:extra + 1]] if timed
+        # (the results `value`'s path wrote into host memory)
+        batches = ([(rot[k], torch.from_numpy(h_perm[k * n_slice:(k + 1) * n_slice]),
+                     torch.from_numpy(h_err[k * n_slice:(k + 1) * n_slice])) for k in timed[:extra + 1]] if timed
                    else [(items, perm.clone(), err.clone())])
         extra = max(0, extra + 1 - len(batches))
         for k in range(extra):
             it = WL.checks(args.batch, 5000 + k)
-            pk = torch.zeros_like(perm)
-            ek = torch.zeros_like(err)
+            pk = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
+            ek = torch.zeros(args.batch, dtype=torch.int32, device=dev)
             eng.check_bulk_device(it.data_ptr(), args.batch, pk.data_ptr(), ek.data_ptr(), stream=stream)
             batches.append((it, pk, ek))
         torch.cuda.synchronize()
@@ -890,7 +938,8 @@ def main():
                 bad = np.nonzero(~ok)[0]
                 # the same batch again, synchronously: does the engine agree the second time?
                 it = batches[bi][0]
-                pk, ek = torch.zeros_like(perm), torch.zeros_like(err)
+                pk = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
+                ek = torch.zeros(args.batch, dtype=torch.int32, device=dev)
                 eng.check_bulk_device(it.data_ptr(), args.batch, pk.data_ptr(), ek.data_ptr(), stream=stream)
                 torch.cuda.synchronize()
                 rp, re_ = pk.cpu().numpy(), ek.cpu().numpy()
@@ -1015,6 +1064,10 @@ def main():
             **({"baseline_step": baseline_step} if baseline_step else {}),
             **({"weak_scaling": weak} if weak else {}),
             **({"host_buffers": host_rate} if host_rate else {}),
+            **({"device_resident": device_resident} if device_resident else {}),
+            **({"pcie": pcie} if pcie else {}),
+            **({"host_equals_device_resident": same_results} if same_results is not None else {}),
+            "host_placement": placement,
             "oracle_agreement": agree,
             **({"disagreements": disagree} if disagree else {}),
             "result_mix": {"HAS": int((res == 2).sum()), "NO": int((res == 1).sum()),

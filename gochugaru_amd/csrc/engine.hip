@@ -210,6 +210,7 @@ struct Workspace {
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
+  bool b_validate = false;    // host items read in place: the join checks their context slots
   void* aql_kernarg = nullptr;  // aql.inc: kernarg block of the dispatched join (pinned host memory, or VRAM)
   bool aql_devargs = false;     // ... in VRAM (aql.inc AqlState::devargs)
   uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
@@ -2254,6 +2255,18 @@ static void launch_wave_bundles(Engine& e, Workspace& w, const Ctx& c, const Bun
 // Stage A of a bundle batch (n <= max_batch): the persistent wave-bundle kernel over every
 // check, then — for a host batch — the copy of the results into the pinned staging, and the
 // publication the host spins on. Nothing waits here.
+// The request check of host items that no join reads in place (include/gck.h: a context_slot
+// beyond the call's contexts is GCK_E_INVALID_ARGUMENT).
+static void slot_error(uint32_t i, uint32_t slot, uint32_t limit) {
+  throw Error(GCK_E_INVALID_ARGUMENT, "item " + std::to_string(i) + ": context_slot " + std::to_string(slot) +
+                                          " beyond the " + std::to_string(limit) + " contexts given");
+}
+
+static void validate_slots(const gck_item* items, uint32_t n, uint32_t limit) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (items[i].context_slot > limit) slot_error(i, items[i].context_slot, limit);
+}
+
 // Stage A of a batch begins with the label join (labels.inc) rather than the closure join.
 static bool label_join_on(const Engine& e) {
   const DeviceSnapshot& ds = *e.dev;
@@ -2345,6 +2358,10 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.cav_n = ds.n_cav;
       j.cav_rows = rows;
     }
+    if (w.b_validate) {
+      j.bad_slot = &w.ctr->bad_slot;
+      j.slot_limit = w.cav.n_given;
+    }
     if (self_pub) {  // self-published (see the closure join below)
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
@@ -2394,6 +2411,10 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.cj_o_meta;
     j.o_entries = ds.cj_o_entries;
     j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
+    if (w.b_validate) {
+      j.bad_slot = &w.ctr->bad_slot;
+      j.slot_limit = w.cav.n_given;
+    }
     // self-published as the label join (a host-side stream query or synchronisation per batch
     // instead costs ~10 us, 11 G -> 3-5 G checks/s)
     if (self_pub) {
@@ -2463,6 +2484,10 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   wait_published(w, st, w.b_seq);
   add_counters(e, w, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
+  if (w.h_ctr->bad_slot) {  // (a zero-copy batch's join found a context slot out of range)
+    const uint32_t i = 0xFFFFFFFFu - w.h_ctr->bad_slot;
+    slot_error(i, i < n ? d_items[i].context_slot : 0u, w.cav.n_given);
+  }
   const bool profile = w.b_timed;
   float ms = 0.f, bm = 0.f, gm = 0.f;
   if (w.b_timed && w.b_aql) ms = aql_elapsed_ms(*e.aql, w);  // (its queue's dispatch timestamps)
@@ -2837,8 +2862,12 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   // (GCK_AQL=0, a profiled batch): the DMA path below.
   w.b_copy_perm = nullptr;
   w.b_copy_err = nullptr;
-  if (host && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) &&
-      (e.dev->d_cj || e.dev->d_lj)) {
+  w.b_validate = false;
+  const bool join = label_join_on(e) || (e.dev->d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE));
+  if (host && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) && join) {
+    // the join reads every item once, in place: it also checks the context slots (no host pass
+    // over the items on the submitting thread)
+    w.b_validate = true;
     const bool pin_in = host_pinned(e, items, (size_t)n * sizeof(gck_item));
     const bool pin_out = host_pinned(e, perm, n) && host_pinned(e, err, (size_t)n * 4);
     // pageable buffers go through the workspace's pinned staging — one host copy each way — and
@@ -2857,6 +2886,7 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
     }
   }
   if (host) {
+    validate_slots(items, n, w.cav.n_given);
     // items: a DMA straight from the caller's buffer when it is pinned (gck_host_alloc), else
     // through the workspace's pinned staging (one host copy, one DMA); results likewise
     if (host_pinned(e, items, (size_t)n * sizeof(gck_item))) {

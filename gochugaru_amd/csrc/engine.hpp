@@ -140,6 +140,7 @@ struct UpdateGroup {
 // caveat_passes).
 struct CavCall {
   uint32_t n_ctx = 0;             // contexts of the call (0: none, or no partial instance)
+  uint32_t n_given = 0;           // contexts the call gave (a host item's context_slot must not exceed it)
   // dense: rows x n_dist outcomes (0 false, 1 true, 2 partial, 3 error) over the distinct
   // context texts, and each slot's distinct text; empty with n_ctx > 0: lazy
   std::vector<uint8_t> dense;

@@ -67,6 +67,7 @@ constexpr size_t kDensePairs = 4096;  // evaluations done eagerly
 
 static CavCall caveat_call(Engine& e, const char* const* ctxs, const size_t* lens, size_t n_ctx) {
   CavCall c;
+  c.n_given = (uint32_t)std::min<size_t>(n_ctx, 0xFFFFFFFFu);
   const size_t rows = e.caveat_partial.size();
   if (n_ctx == 0 || rows == 0) return c;
   REQUIRE(n_ctx < (1ull << 31), GCK_E_INVALID_ARGUMENT, "too many check contexts");
@@ -685,11 +686,12 @@ static void check_request(Engine& e, const gck_consistency* cs, const gck_item* 
   REQUIRE(n_contexts < 0xFFFFFFFFull, GCK_E_INVALID_ARGUMENT, "too many contexts");
   REQUIRE(e.part_world <= 1, GCK_E_STATE, "partitioned engine: use gck_part_* (every rank together)");
   check_consistency(e, cs);
-  if (host_items)
-    for (size_t i = 0; i < n; ++i)
-      REQUIRE(items[i].context_slot <= n_contexts, GCK_E_INVALID_ARGUMENT,
-              "item " + std::to_string(i) + ": context_slot " + std::to_string(items[i].context_slot) +
-                  " beyond the " + std::to_string(n_contexts) + " contexts given");
+  // (a host item's context_slot is validated by its batch: the join of a zero-copy batch checks
+  // every item it reads, the others are scanned before they are staged — engine.hip submit_batch;
+  // a scan here read every host item once more on the submitting thread, ~27 us per 64K batch)
+  (void)items;
+  (void)n;
+  (void)host_items;
 }
 
 int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,

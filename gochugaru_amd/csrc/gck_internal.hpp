@@ -200,6 +200,8 @@ struct DevCounters {  // device-side counters, reset per level where noted
                                     // the slot-path count is n - deferred - this, on the host)
   unsigned int cav_requests;        // (caveat instance, check context) pairs recorded for evaluation
   unsigned int cav_errors;          // touched pairs whose evaluation failed
+  unsigned int bad_slot;            // a host item whose context_slot exceeds the call's contexts (the
+                                    // joins validate zero-copy batches): 0xFFFFFFFF - its index, 0 none
 };
 
 }  // namespace gck

@@ -211,6 +211,54 @@ _lib = None
 _DRIVER = None
 
 
+def _cpulist(text: str) -> List[int]:
+    out = []
+    for tok in text.strip().split(","):
+        if tok:
+            a, _, b = tok.partition("-")
+            out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def device_numa_node(device: int = 0) -> Tuple[int, str]:
+    """The NUMA node of the GPU's PCIe root (sysfs), and its PCI address; -1 when unknown."""
+    import torch
+    p = torch.cuda.get_device_properties(device)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    try:
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            return int(f.read().strip()), bdf
+    except (OSError, ValueError):
+        return -1, bdf
+
+
+def pin_to_device_node(device: int = 0) -> dict:
+    """Runs the calling process on the CPUs of the GPU's NUMA node (those of them it may use).
+
+    A host batch's items are read by the GPU across PCIe right after the submitting thread wrote
+    them: from a thread on the other socket every line is snooped out of a remote cache, and
+    the copy engines and kernels read host memory ~10 % slower (tools/pcie_probe: zero-copy reads
+    36 vs 40 GB/s, DMA 28-32 vs 41 GB/s). Pinned buffers already come from the GPU's node
+    (hipHostMalloc follows the device). Returns what was done, for the bench line."""
+    node, bdf = device_numa_node(device)
+    allowed = sorted(os.sched_getaffinity(0))
+    info = {"gpu_bdf": bdf, "gpu_numa_node": node, "cpus_allowed": len(allowed), "pinned": False}
+    if node < 0:
+        return info
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            local = set(_cpulist(f.read()))
+    except OSError:
+        return info
+    use = [c for c in allowed if c in local]
+    if use and len(use) < len(allowed):
+        os.sched_setaffinity(0, use)
+        info.update(pinned=True, cpus_used=len(use))
+    elif use:
+        info.update(cpus_used=len(use))
+    return info
+
+
 def _driver():
     """libgck_driver.so (csrc/driver.cpp): the compiled submit/wait loop bench.py times through."""
     global _DRIVER
