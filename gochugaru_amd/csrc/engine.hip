@@ -3120,7 +3120,7 @@ static Workspace& part_workspace(Engine& e) {
 #include "partition.inc"
 #include "lookup.inc"
 
-static PartState& part_state(Workspace& w) {
+static PartState& part_state(Workspace& w) {  // (caller holds w.m: part_run)
   if (!w.part) w.part = new PartState();
   return *w.part;
 }

@@ -258,6 +258,7 @@ std::vector<HostCSR> build_csrs(Engine& e);
 // Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
 void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
 std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n);
+void validate_updates(const Engine& e, const gck_update* ups, size_t n);
 
 // engine.hip
 int device_init(Engine& e);

@@ -263,9 +263,18 @@ int gck_intern(gck_engine* ge, uint16_t type, const char* const* ids, const uint
     REQUIRE(type < sc.types.size(), GCK_E_INVALID_ARGUMENT, "unknown type id");
     REQUIRE(n == 0 || (ids && lens && out_ids), GCK_E_INVALID_ARGUMENT, "null argument");
     const bool create = flags & GCK_INTERN_CREATE;
+    // creating ids is a write of the interner: it takes the writer lock as every writer does, so
+    // that no Watch batch is between its interner mark and its rollback meanwhile (a text batch
+    // that fails truncates the interner to the counts it recorded, gck_apply_updates_text)
+    std::unique_lock<std::mutex> wlk(e.writer_mu, std::defer_lock);
     std::unique_lock<std::shared_mutex> lk(e.mu, std::defer_lock);
     std::shared_lock<std::shared_mutex> slk(e.mu, std::defer_lock);
-    if (create) lk.lock(); else slk.lock();
+    if (create) {
+      wlk.lock();
+      lk.lock();
+    } else {
+      slk.lock();
+    }
     TypeInterner& ti = e.interner[type];
     std::string key;
     for (size_t i = 0; i < n; ++i) {
@@ -520,6 +529,9 @@ static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, ui
   PhaseClock pc("watch");
   std::vector<gck_update> mine;
   if (e.part_world > 1) {  // partitioned graph: the updates of what this rank keeps (part_keep)
+    // the whole batch validated first, as every rank validates it: an update another rank would
+    // keep and reject fails the batch here too (every rank stays at the old revision)
+    validate_updates(e, ups, n);
     for (size_t i = 0; i < n; ++i) {
       const gck_tuple& t = ups[i].tuple;
       if (part_keep(e, t.relation, t.resource_id, t.subject_id, t.subject_relation)) mine.push_back(ups[i]);

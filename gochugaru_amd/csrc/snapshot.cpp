@@ -331,6 +331,32 @@ void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck
   });
 }
 
+// The validation group_updates does, alone: a partitioned engine validates the whole batch before
+// it keeps its own updates (part_keep), so that an update only one rank keeps — an unknown
+// relation, a subject the schema disallows, an id never interned — is refused by every rank and
+// no rank moves to the new revision without the others. One schema check per (resource type,
+// kind, wildcard) combination, as group_updates makes them.
+void validate_updates(const Engine& e, const gck_update* ups, size_t n) {
+  std::vector<uint64_t> seen;
+  for (size_t i = 0; i < n; ++i) {
+    const gck_update& u = ups[i];
+    if (u.op != GCK_UPDATE_CREATE && u.op != GCK_UPDATE_TOUCH && u.op != GCK_UPDATE_DELETE)
+      throw Error(GCK_E_INVALID_ARGUMENT, "unknown update operation " + std::to_string(u.op));
+    const gck_tuple& t = u.tuple;
+    const uint64_t combo = ((uint64_t)(t.resource_type & 0x7FFF) << 48) | ((uint64_t)t.relation << 32) |
+                           ((uint64_t)t.subject_type << 16) | t.subject_relation |
+                           (t.subject_id == kWildcard ? (1ull << 63) : 0ull);
+    if (std::find(seen.begin(), seen.end(), combo) == seen.end()) {
+      validate_tuple(e, t);
+      seen.push_back(combo);
+    } else if (t.resource_id >= e.interner[t.resource_type].count ||
+               (t.subject_id != kWildcard && t.subject_id >= e.interner[t.subject_type].count) ||
+               t.caveat >= e.caveat_instances.size()) {
+      validate_tuple(e, t);  // (raises the error)
+    }
+  }
+}
+
 // Validates the updates and groups them per (relation, subject type, subject relation); within a
 // group the last write per (object, subject) wins (the order of the Watch stream). Groups come
 // out in ascending (relation, subject type, subject relation) order, keys ascending: a stable

@@ -38,8 +38,8 @@ def _hip():
         except OSError:
             pass
         h = ctypes.CDLL(path)
-        h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        h.hipMemcpy.restype = ctypes.c_int
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        h.hipMemcpyAsync.restype = ctypes.c_int
         h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
         h.hipStreamSynchronize.restype = ctypes.c_int
         _HIP = h
@@ -73,13 +73,18 @@ class GlooTransport:
             if rc != 0:
                 raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
 
-    def _copy(self, dst: int, src: int, n: int):
+    def _copy(self, dst: int, src: int, n: int, stream):
         if n == 0:
             return
         if self.device:
-            rc = _hip().hipMemcpy(dst, src, n, 4)  # hipMemcpyDefault: host or device on either side
+            # on the engine's stream, then waited for: the engine's next kernels on that stream are
+            # ordered after the copy, and the host buffer may be reused once this returns (a
+            # synchronous hipMemcpy runs on the null stream, which a non-blocking stream does not
+            # wait for, and may return before a pageable upload has landed)
+            rc = _hip().hipMemcpyAsync(dst, src, n, 4, stream)  # hipMemcpyDefault: either side
             if rc != 0:
-                raise RuntimeError(f"hipMemcpy failed ({rc})")
+                raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+            self._sync(stream)
         else:
             ctypes.memmove(dst, src, n)
 
@@ -91,9 +96,9 @@ class GlooTransport:
             self._sync(stream)
             hs = torch.empty(sum(sb), dtype=torch.uint8)
             hr = torch.empty(sum(rb), dtype=torch.uint8)
-            self._copy(hs.data_ptr(), send, sum(sb))
+            self._copy(hs.data_ptr(), send, sum(sb), stream)
             self.dist.all_to_all_single(hr, hs, output_split_sizes=rb, input_split_sizes=sb, group=self.group)
-            self._copy(recv, hr.data_ptr(), sum(rb))
+            self._copy(recv, hr.data_ptr(), sum(rb), stream)
             self.calls["alltoallv"] += 1
             self.calls["bytes"] += sum(sb)
             return 0
@@ -106,9 +111,9 @@ class GlooTransport:
             torch = self.torch
             self._sync(stream)
             h = torch.empty(int(n), dtype=torch.uint8)
-            self._copy(h.data_ptr(), buf, int(n))
+            self._copy(h.data_ptr(), buf, int(n), stream)
             self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX, group=self.group)
-            self._copy(buf, h.data_ptr(), int(n))
+            self._copy(buf, h.data_ptr(), int(n), stream)
             self.calls["allreduce_max_u8"] += 1
             return 0
         except Exception:

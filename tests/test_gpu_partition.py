@@ -237,3 +237,45 @@ def test_rccl_single_rank_matches_oracle(family, seed):
     perm2, err2 = pc.check(d_items, len(items), now_us=gen.NOW_US)  # the communicator is reused
     assert perm2.cpu().tolist() == perm.cpu().tolist() and err2.cpu().tolist() == err.cpu().tolist()
     e.close()
+
+
+def test_invalid_update_rejected_on_every_rank():
+    """A Watch batch with an update only one rank keeps (part_keep) and the schema rejects: every
+    rank refuses the whole batch and stays at the old revision (each validates the batch before
+    it keeps its own updates, gck_api.cpp apply_updates), so no rank moves ahead of the others.
+    The engines of both ranks live in this process: applying a batch needs no exchange."""
+    schema, tuples, _ = gen.FAMILIES["gdocs"](2)
+    engines = []
+    for r in range(2):
+        e = E.Engine(device=0)
+        e.set_partition(r, 2)
+        e.load_schema(schema)
+        e.load_snapshot_text(1, "\n".join(tuples))
+        engines.append(e)
+    e0 = engines[0]
+    t_doc, t_user, t_folder = e0.type_id("doc"), e0.type_id("user"), e0.type_id("folder")
+    viewer = e0.relation_id(t_doc, "viewer")
+    n_docs = e0.object_count(t_doc)
+    doc0 = next(d for d in range(n_docs) if E.partition_owner(d, 2) == 0)
+    doc1 = next(d for d in range(n_docs) if E.partition_owner(d, 2) == 1)
+
+    def update(doc, stype, sid):
+        u = np.zeros(1, dtype=E.UPDATE_DTYPE)
+        u["op"] = E.UPDATE_CREATE
+        t = u["tuple"]
+        t["resource_type"], t["relation"], t["resource_id"] = t_doc, viewer, doc
+        t["subject_type"], t["subject_relation"], t["subject_id"] = stype, E.ELLIPSIS, sid
+        return u
+    good = update(doc0, t_user, 0)                # kept by rank 0 only: valid
+    bad = update(doc1, t_folder, 0)               # kept by rank 1 only: doc#viewer allows no folder
+    batch = np.concatenate([good, bad])
+    for r, e in enumerate(engines):
+        with pytest.raises(E.GckError) as ei:
+            e.apply_updates(2, batch)
+        assert ei.value.code == E.GCK_E_INVALID_ARGUMENT, (r, ei.value)
+        assert e.revision == 1, (r, e.revision)
+    for e in engines:  # the valid update alone applies on both ranks
+        e.apply_updates(2, good)
+        assert e.revision == 2
+    for e in engines:
+        e.close()
