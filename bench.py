@@ -423,7 +423,9 @@ def main():
         # config 5: per step one Watch batch (pre-generated: the stream's arrivals) then one check
         # batch with contexts, at the revision the batch moved the snapshot to
         from tests.synth_configs import CONTEXTS
-        items = WL.checks(args.batch, 1000 + rank)
+        # every step its own check batch (no step re-reads a batch another step left in the caches)
+        m_rot = [WL.checks(args.batch, 1000 + 100003 * rank + k) for k in range(args.warm + args.steps)]
+        items = m_rot[0]
         perm = torch.zeros(args.batch, dtype=torch.uint8, device=dev)
         err = torch.zeros(args.batch, dtype=torch.int32, device=dev)
         # The check batch is submitted and left running: the next step's Watch batch validates,
@@ -442,8 +444,10 @@ def main():
             rev["k"] += 1
             rev["apply_s"] += time.perf_counter() - t_a
             t_s = time.perf_counter()
-            b = eng.submit(items.data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), device=True,
-                           stream=stream, contexts=m_ctx)
+            # on the engine's streams: the label join with its caveat plane is dispatched into the
+            # engine's HSA queues (aql.inc), the contexts' Ctx in the kernarg block
+            b = eng.submit(m_rot[rev["k"] - 1].data_ptr(), args.batch, perm.data_ptr(), err.data_ptr(), device=True,
+                           stream=stream, contexts=m_ctx, engine_stream=bool(args.engine_streams))
             rev["submit_s"] += time.perf_counter() - t_s
             if rev["pending"] is not None:
                 t_w = time.perf_counter()
@@ -658,6 +662,8 @@ def main():
                 for k in range(args.warm, args.warm + args.steps))
     if WL.kind == "quota":
         items, (perm, err) = q_rot[args.warm][0], q_out[args.warm]
+    if WL.kind == "mixed":  # the last step's batch: checked on the final snapshot, as the oracle is
+        items = m_rot[rev["k"] - 1]
     st = eng.stats()
     # per-launch time of the dominant kernel, alone on the GPU: the timed batches again, one at a
     # time, device-resident (the kernel's own HBM roofline, without the PCIe reads of `value`'s

@@ -139,6 +139,15 @@ struct DeviceSnapshot {
   uint32_t* lj_dirty = nullptr;
   uint64_t lj_dirty_n = 0;       // changed grants marked (an upper bound of the dirty subjects)
   uint32_t lj_users = 0;
+  // the arrow forest of the label roots' resources (labels.inc lj_forest: every object the
+  // flattening of a resource visits is an ancestor of it): per vertex (pre, end), per type its
+  // first vertex (kNone: not in the forest); null: no forest, a dirty subject's checks all defer
+  uint32_t* lj_af = nullptr;
+  std::vector<uint32_t> lj_af_base, lj_af_rows;
+  std::vector<std::pair<uint32_t, uint16_t>> lj_dtype;  // direct-grant CSR -> the type of its rows
+  // per dirty subject the forest intervals of the objects whose grants of it changed (kDovWords
+  // each, labels.inc): its checks defer only when one holds the resource (shared like lj_dirty)
+  uint32_t* lj_dov = nullptr;
   std::vector<void*> adopt_h;    // arrays of the current snapshot this one takes over at publish
                                  // (device_publish: contiguous ones move to hallocs, others to allocs)
   std::vector<SlotRec> slot_recs;
@@ -1601,7 +1610,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
         part_filter_device(e, *ds, h, d, ne);
         b.n_edges = ne;
         e.n_tuples -= std::min<uint64_t>(e.n_tuples, loaded - ne);  // (the engine counts what it holds)
-        if (ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+        if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
         }
@@ -2348,6 +2357,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.table_bytes = (uint32_t)((ds.lj_host.size() + 3) & ~(size_t)3);
     j.o_meta = ds.lj_o_meta;
     j.dirty = ds.lj_dirty;
+    j.dov = ds.lj_dov;
     bool cl = false;
     const bool cav = ds.lj_cav && w.cav_on;  // caveated pairs decided under the check contexts (cav_state)
     if (cav) {

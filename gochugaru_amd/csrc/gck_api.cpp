@@ -856,7 +856,11 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
     e.part_world = world;
     e.part_set = true;
     partition_rules(e);
-    if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR;  // both need the whole graph
+    // the bundles and the bidirectional search need the whole graph; the membership indexes serve
+    // the bundles: a partitioned rank's checks are decided by the partitioned label join from the
+    // slots, and its level loop (what the join leaves) finds a subject in a row by binary search —
+    // at 1e9 tuples the index of the kept memberships alone would be 13 of a rank's 29 GB
+    if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR | GCK_FLAG_NO_MHASH;
   });
 }
 
