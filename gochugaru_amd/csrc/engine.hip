@@ -367,6 +367,10 @@ struct Ctx {
   // partitioned graph the end of this rank's own id range (partition.inc part_loop)
   uint32_t q_hi, j_hi;
   uint32_t force_exact;  // every root runs exact-depth (partitioned graphs: no global heights)
+  // partitioned graphs: per node 1 for the nodes of a hub (group#member and the relations it
+  // unions): their entries go to the owner of the check's subject, which holds the subject's
+  // direct memberships and the replicated hierarchy (partition.inc part_dest); null: by object
+  const uint8_t* part_sub;
 };
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -447,6 +451,15 @@ __device__ __forceinline__ void set_found(const Ctx& c, uint32_t q, uint32_t con
   atomicOr(&c.queries[q].flags, (cond & kCondBit) ? (uint32_t)QF_FOUND_C : (uint32_t)QF_FOUND_Y);
 }
 
+// The rank that expands an entry of a partitioned graph: the owner of its object's rows, or — at a
+// hub's nodes, whose userset tuples every rank holds and whose direct tuples only the subject's
+// owner does — the owner of the check's subject (engine.hpp part_keep).
+__device__ __forceinline__ uint32_t part_dest(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node) {
+  if (c.part_sub && c.part_sub[node])
+    return part_owner(c.ck_items[c.queries[q].check].subject_id, c.world);
+  return part_owner(obj, c.world);
+}
+
 __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t obj, uint16_t node,
                                            uint32_t depth, uint32_t cond) {
   if (cond & kExactBit) {  // exact-depth: one entry per (vertex, depth); never a cond path
@@ -457,10 +470,10 @@ __device__ __forceinline__ void push_entry(const Ctx& c, uint32_t q, uint32_t ob
   }
   Entry* dst = c.next;
   unsigned idx;
-  if (c.world > 1 && part_owner(obj, c.world) != c.rank) {
-    // another rank owns obj's rows: exchanged after this level (the visited key above also
-    // stops this rank from sending the same entry twice)
-    const uint32_t d = part_owner(obj, c.world);
+  if (c.world > 1 && part_dest(c, q, obj, node) != c.rank) {
+    // another rank holds what the entry reads: exchanged after this level (the visited key
+    // above also stops this rank from sending the same entry twice)
+    const uint32_t d = part_dest(c, q, obj, node);
     idx = atomicAdd(&c.out_cnt[d], 1u);
     if (idx >= c.out_cap) {
       atomicOr(&c.ctr->overflow, 2u);
@@ -1567,6 +1580,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
   PhaseClock pc(delta ? "relink" : "upload");
   device_init(e);
   HIP_OK(hipSetDevice(e.device));
+  pc.mark("init");
   Schema& sc = *e.schema;
   auto* ds = new DeviceSnapshot();
   try {
@@ -1650,7 +1664,13 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
       info.push_back({ne, h.stype});
       ds->base.push_back(b);
     }
-    HIP_OK(hipDeviceSynchronize());
+    // the uploads, indexes and (a Watch batch) the merge are on the null stream: wait for those
+    // only — a device-wide synchronisation would also wait for the check batches running on the
+    // engine's non-blocking streams beside the build (config 5: ~55 us of a 0.29 ms Watch batch)
+    pc.mark("csr_loop");
+    if (delta) HIP_OK(hipStreamSynchronize(nullptr));
+    else HIP_OK(hipDeviceSynchronize());
+    pc.mark("csr_sync");
     // link the node program to the CSR table
     std::vector<DevItem> items = sc.items;
     for (size_t i = 0; i < items.size(); ++i) {
@@ -2015,6 +2035,7 @@ static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
   c.q_hi = c.query_cap;
   c.j_hi = c.join_cap;
   c.force_exact = 0;
+  c.part_sub = nullptr;
   c.max_depth = e.cfg.max_depth ? e.cfg.max_depth : 50;
   if (deep) {  // exact-depth checks key their entries by depth (make_key)
     const uint32_t db = ceil_log2((uint64_t)c.max_depth + 1);
@@ -2451,7 +2472,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       Ctx c;
       CjArgs j;
     } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
-    static_assert(offsetof(decltype(cj_args), j) == 336, "k_closure_join kernarg layout (Ctx, CjArgs)");
+    static_assert(offsetof(decltype(cj_args), j) == 344, "k_closure_join kernarg layout (Ctx, CjArgs)");
     // (half slots: the first 32 B of each resource slot, closure.inc HALF)
     if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
                         sizeof(cj_args), grid.x)) {

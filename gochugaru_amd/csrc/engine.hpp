@@ -92,6 +92,11 @@ struct TypeInterner {
   std::unordered_map<std::string, uint32_t> ids;
   std::vector<std::string> names;  // names[id] ("" for anonymous reserved ids)
   uint32_t count = 0;              // ids [0, count) exist
+  // a partitioned graph (partition.inc part_intern): the names this rank owns get ids
+  // local * world + rank in order; the names of other ranks' objects it needs are kept with the
+  // ids their owners gave, id -> name here (names[] would span the whole id space)
+  uint32_t local = 0;
+  std::unordered_map<uint32_t, std::string> rev;
 };
 
 // ---- snapshot staging -----------------------------------------------------------------------
@@ -133,6 +138,15 @@ struct UpdateGroup {
   std::vector<int64_t> exp_us;           // expiration per key (0 = never)
 };
 
+// snapshot.cpp group_updates' storage, reused batch after batch (a Watch batch holds it under the
+// writer lock): per kind its records, the bucket pass's buffers, and the groups it returns.
+struct GroupBuffers {
+  std::vector<std::vector<uint64_t>> recs;
+  std::vector<uint64_t> tmp, kinds;
+  std::vector<uint32_t> cnt, bucket;
+  std::vector<UpdateGroup> out;
+};
+
 // The check-time caveat contexts of one call (CheckBulkPermissionsRequestItem.Context,
 // client/client.go:257) and how their outcomes reach the device: a dense table of every partial
 // caveat instance x context when that is small, otherwise lazily — the walk records the pairs it
@@ -162,6 +176,7 @@ struct Engine {
   // the schema's hub nodes and the relations of their hierarchy (labels.inc partition_rules): what
   // a rank keeps beyond the rows it owns (part_keep)
   std::vector<char> part_hub_node, part_hub_rel;
+  std::vector<uint8_t> part_sub_node;  // the hubs' nodes (partition.inc part_dest)
   bool device_ready = false;
   std::shared_mutex mu;  // shared: checks (and a Watch batch's build); exclusive: schema/snapshot
   std::mutex writer_mu;  // one writer at a time (gck_api.cpp WriterLock; a Watch batch holds it throughout)
@@ -205,7 +220,7 @@ struct Engine {
   size_t delta_scratch_cap = 0;
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
-  std::vector<uint64_t> group_scratch;  // group_updates' sort buffers, kept across Watch batches
+  GroupBuffers group_buf;  // group_updates' records and groups, kept across Watch batches
   // merged-CSR arrays of retired snapshots kept for the next Watch batch's merge (engine.hip
   // ralloc / retire_array): bytes -> array, and every array ralloc handed out -> its bytes
   std::multimap<size_t, void*> recycle;
@@ -235,19 +250,30 @@ struct PhaseClock {
 };
 
 // Partitioned graphs: does rank e.part_rank keep the tuple rel(obj) <- (sid, srel)?
-// Its own rows (part_owner(obj)); and of a hub relation (partition_rules) every userset and
-// wildcard tuple — the replicated hierarchy — and the tuples of the subjects it owns (their user
-// slots). Every ingest path applies it (staging, gck_load_csr, Watch batches) after interning, so
+// Its own rows (part_owner(obj)); of a hub relation (partition_rules) instead every userset and
+// wildcard tuple — the replicated hierarchy — and the direct tuples of the subjects it owns (their
+// user slots, and what the level loop reads at a hub node, partition.inc part_dest). Every ingest path applies it (staging, gck_load_csr, Watch batches) after interning, so
 // that ids and caveat instances stay the same on every rank.
 inline bool part_keep(const Engine& e, uint16_t rel, uint32_t obj, uint32_t sid, uint16_t srel) {
-  if (e.part_world <= 1 || part_owner(obj, e.part_world) == e.part_rank) return true;
-  if (rel >= e.part_hub_rel.size() || !e.part_hub_rel[rel]) return false;
+  if (e.part_world <= 1) return true;
+  if (rel >= e.part_hub_rel.size() || !e.part_hub_rel[rel]) return part_owner(obj, e.part_world) == e.part_rank;
+  // a hub relation: the hierarchy everywhere, a direct tuple with its subject's owner only (the
+  // level loop expands hub nodes there: partition.inc part_dest)
   return srel != kEllipsis || sid == kWildcard || part_owner(sid, e.part_world) == e.part_rank;
 }
 void partition_rules(Engine& e);  // labels.inc: e.part_hub_node / part_hub_rel from the schema
 
 // snapshot.cpp
 void add_tuples_text(Engine& e, const char* text, size_t len);
+struct TupleNames {  // a relationship line with its object ids still names (parse_tuple_names)
+  uint16_t rt = 0, rel = 0, st = 0, srel = kEllipsis;
+  std::string rid, sid;
+  uint32_t cav = 0;
+  int64_t exp = 0;
+};
+TupleNames parse_tuple_names(Engine& e, const std::string& line);
+std::vector<TupleNames> parse_tuples_text(Engine& e, const char* text, size_t len);
+void stage_tuple(Engine& e, const gck_tuple& t);
 // gck_api.cpp: caveat instances (a caveat name + stored context)
 void reset_caveats(Engine& e);
 uint32_t add_caveat_instance(Engine& e, const std::string& name, const std::string& json);
@@ -257,7 +283,7 @@ void load_snapshot_file(Engine& e, const std::string& path);
 std::vector<HostCSR> build_csrs(Engine& e);
 // Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
 void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
-std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n);
+const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, size_t n);
 void validate_updates(const Engine& e, const gck_update* ups, size_t n);
 
 // engine.hip
@@ -331,6 +357,10 @@ void part_check(Engine& e, const gck_item* d_items, size_t n, int64_t now_us, ui
                 void* stream);
 void part_check_with(Engine& e, const gck_transport& t, const gck_item* d_items, size_t n, int64_t now_us,
                      uint8_t* d_perm, int32_t* d_err, void* stream);
+uint32_t part_owner_name(uint16_t type, const char* s, size_t len, uint32_t world);
+void part_intern(Engine& e, const gck_transport& t, const uint16_t* types, const char* const* names,
+                 const uint32_t* lens, size_t n, bool create, uint32_t* out);
+void part_add_tuples_text(Engine& e, const gck_transport& t, const char* text, size_t len);
 void part_comm_free(Engine& e);
 void device_free(Engine& e);
 

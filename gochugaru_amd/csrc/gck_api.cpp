@@ -287,6 +287,9 @@ int gck_intern(gck_engine* ge, uint16_t type, const char* const* ids, const uint
       if (it != ti.ids.end()) {
         out_ids[i] = it->second;
       } else if (create) {
+        // (a partitioned graph: only a name's owner gives it an id, gck_part_intern_with)
+        REQUIRE(e.part_world <= 1, GCK_E_STATE, "a partitioned engine interns a new name through its owner rank "
+                                                "(gck_part_intern_with): '" + key + "'");
         REQUIRE(ti.count < GCK_ID_ABSENT, GCK_E_CAPACITY, "too many objects of one type");
         uint32_t id = ti.count++;
         ti.ids.emplace(key, id);
@@ -325,7 +328,10 @@ int gck_object_name(gck_engine* ge, uint16_t type, uint32_t id, char* buf, size_
     REQUIRE(type < need_schema(e).types.size(), GCK_E_INVALID_ARGUMENT, "bad type");
     TypeInterner& ti = e.interner[type];
     REQUIRE(id < ti.count, GCK_E_NOT_FOUND, "unknown object id");
-    std::string nm = id < ti.names.size() && !ti.names[id].empty() ? ti.names[id] : std::to_string(id);
+    auto rv = ti.rev.find(id);
+    std::string nm = id < ti.names.size() && !ti.names[id].empty() ? ti.names[id]
+                     : rv != ti.rev.end()                           ? rv->second
+                                                                    : std::to_string(id);
     if (out_len) *out_len = nm.size();
     if (buf && cap) {
       size_t k = std::min(cap - 1, nm.size());
@@ -542,12 +548,11 @@ static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, ui
   // validation and grouping read the interner and the schema, which only writers change (and
   // writer_mu holds them off): beside the checks too
   WatchBuild wb;
-  std::vector<UpdateGroup> groups;
   lk.unlock();
   bool built = false;
   try {
     std::shared_lock<std::shared_mutex> sl(e.mu);  // (checks run on the current snapshot meanwhile)
-    groups = group_updates(e, ups, n);
+    const std::vector<UpdateGroup>& groups = group_updates(e, ups, n);  // (the engine's, until the next batch)
     pc.mark("group");
     if (!groups.empty()) device_apply_build(e, groups, wb);
     built = true;
@@ -861,6 +866,44 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
     // slots, and its level loop (what the join leaves) finds a subject in a row by binary search —
     // at 1e9 tuples the index of the kept memberships alone would be 13 of a rank's 29 GB
     if (world > 1) e.cfg.flags |= GCK_FLAG_NO_BUNDLE | GCK_FLAG_NO_BIDIR | GCK_FLAG_NO_MHASH;
+  });
+}
+
+uint32_t gck_partition_owner_name(uint16_t type, const char* name, size_t len, uint32_t world) {
+  return part_owner_name(type, name ? name : "", name ? len : 0, world);
+}
+
+int gck_part_intern_with(gck_engine* ge, const gck_transport* t, const uint16_t* types, const char* const* names,
+                         const uint32_t* lens, size_t n, uint32_t flags, uint32_t* out_ids) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(t, GCK_E_INVALID_ARGUMENT, "null transport");
+    REQUIRE(n == 0 || (types && names && lens && out_ids), GCK_E_INVALID_ARGUMENT, "null argument");
+    WriterLock lk(e);  // (the interner changes; every rank's call blocks in the exchange together)
+    part_intern(e, *t, types, names, lens, n, (flags & GCK_INTERN_CREATE) != 0, out_ids);
+  });
+}
+
+int gck_part_add_tuples_text_with(gck_engine* ge, const gck_transport* t, const char* text, size_t len) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(t, GCK_E_INVALID_ARGUMENT, "null transport");
+    REQUIRE(text || !len, GCK_E_INVALID_ARGUMENT, "null text");
+    WriterLock lk(e);
+    REQUIRE(e.staging, GCK_E_STATE, "gck_begin_snapshot first");
+    part_add_tuples_text(e, *t, text, len);
+  });
+}
+
+int gck_interned_names(gck_engine* ge, uint16_t type, uint32_t* out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    REQUIRE(type < need_schema(e).types.size(), GCK_E_INVALID_ARGUMENT, "bad type");
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    *out = (uint32_t)e.interner[type].ids.size();
   });
 }
 

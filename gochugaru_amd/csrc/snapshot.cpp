@@ -76,6 +76,9 @@ uint32_t intern_one(Engine& e, uint16_t type, const std::string& id) {
   TypeInterner& ti = e.interner[type];
   auto it = ti.ids.find(id);
   if (it != ti.ids.end()) return it->second;
+  if (e.part_world > 1)  // (an id here would not be the one the name's owner gives it)
+    throw Error(GCK_E_STATE, "a partitioned engine interns a new name through its owner rank "
+                             "(gck_part_intern_with, gck_part_add_tuples_text_with): '" + id + "'");
   if (ti.count >= kAbsent) throw Error(GCK_E_CAPACITY, "too many objects of one type");
   uint32_t nid = ti.count++;
   ti.ids.emplace(id, nid);
@@ -223,9 +226,12 @@ void for_each_line(const char* text, size_t len, F&& f) {
   }
 }
 
-// One canonical line: type:id#rel@type:id[#rel][caveat[:{json}]][expiration:T]. Interns the
-// ids (creating them) and registers the caveat instance.
-gck_tuple parse_tuple_line(Engine& e, const std::string& line) {
+}  // namespace
+
+// One canonical line: type:id#rel@type:id[#rel][caveat[:{json}]][expiration:T], by name:
+// the types, relations and caveat instance resolved (the instance registered), the object ids
+// left as text (interned by the caller: locally, or by their owners on a partitioned graph).
+TupleNames parse_tuple_names(Engine& e, const std::string& line) {
   const Schema& sc = *e.schema;
   {
     auto bad = [&](const char* why) {
@@ -292,20 +298,43 @@ gck_tuple parse_tuple_line(Engine& e, const std::string& line) {
       if (x < 0) throw bad("unknown subject relation");
       srel = (uint16_t)x;
     }
-    gck_tuple t{};
-    t.resource_type = (uint16_t)rt;
-    t.relation = (uint16_t)rr;
-    t.resource_id = intern_one(e, (uint16_t)rt, rid);
-    t.subject_type = (uint16_t)stt;
-    t.subject_relation = srel;
-    t.subject_id = intern_one(e, (uint16_t)stt, sid);
-    t.caveat = cav_name.empty() ? 0 : add_caveat_instance(e, cav_name, cav_json);
-    t.expires_at_us = exp_us;
+    TupleNames t;
+    t.rt = (uint16_t)rt;
+    t.rel = (uint16_t)rr;
+    t.rid = std::move(rid);
+    t.st = (uint16_t)stt;
+    t.srel = srel;
+    t.sid = std::move(sid);
+    t.cav = cav_name.empty() ? 0 : add_caveat_instance(e, cav_name, cav_json);
+    t.exp = exp_us;
     return t;
   }
 }
 
+namespace {
+
+// The same, its ids interned here (creating them).
+gck_tuple parse_tuple_line(Engine& e, const std::string& line) {
+  TupleNames p = parse_tuple_names(e, line);
+  gck_tuple t{};
+  t.resource_type = p.rt;
+  t.relation = p.rel;
+  t.resource_id = intern_one(e, p.rt, p.rid);
+  t.subject_type = p.st;
+  t.subject_relation = p.srel;
+  t.subject_id = intern_one(e, p.st, p.sid);
+  t.caveat = p.cav;
+  t.expires_at_us = p.exp;
+  return t;
+}
+
 }  // namespace
+
+std::vector<TupleNames> parse_tuples_text(Engine& e, const char* text, size_t len) {
+  std::vector<TupleNames> out;
+  for_each_line(text, len, [&](const std::string& line) { out.push_back(parse_tuple_names(e, line)); });
+  return out;
+}
 
 void add_tuples_text(Engine& e, const char* text, size_t len) {
   for_each_line(text, len, [&](const std::string& line) { stage_tuple(e, parse_tuple_line(e, line)); });
@@ -359,107 +388,109 @@ void validate_updates(const Engine& e, const gck_update* ups, size_t n) {
 
 // Validates the updates and groups them per (relation, subject type, subject relation); within a
 // group the last write per (object, subject) wins (the order of the Watch stream). Groups come
-// out in ascending (relation, subject type, subject relation) order, keys ascending: a stable
-// counting pass into the groups (a batch touches a few kinds), then per group a stable LSD radix
-// sort of the 64-bit (object << 32 | subject) keys in 11-bit digits, digits constant over the
-// group skipped (a comparison sort of a 10K-update batch cost ~0.2 ms of the Watch step).
-std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t n) {
+// out in ascending (relation, subject type, subject relation) order, keys ascending.
+//
+// One pass over the batch validates and stages each update into its kind's record array: a
+// direct-mapped cache of the (resource type, kind, wildcard) combinations whose schema checks
+// passed holds the kind and the object counts the id checks need, so the per-update work is a
+// hash, one well-predicted compare and the bounds checks (a linear search of the combinations
+// mispredicted its exit on every update of a mixed batch). Per kind a stable counting pass on
+// the key's top bits into ~one bucket per update, then an insertion sort of each bucket (a bucket
+// that a skewed batch fills is merge-sorted). Everything lives in Engine::group_buf and is reused
+// batch after batch (fresh vectors cost a 10K-update batch its allocations and page faults).
+const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, size_t n) {
   PhaseClock pc("group");
-  const Schema& sc = *e.schema;
-  // scratch kept by the engine (a Watch batch holds it exclusively): per update its kind index,
-  // then two (key, index) buffers for the radix passes — no allocation or clearing per batch
-  std::vector<uint64_t>& scr = e.group_scratch;
-  if (scr.size() < 5 * n) scr.resize(5 * n);
-  uint32_t* g_of = reinterpret_cast<uint32_t*>(scr.data());
+  if (n >= (1ull << 30)) throw Error(GCK_E_CAPACITY, "a Watch batch holds at most 2^30 updates");
+  GroupBuffers& B = e.group_buf;
   struct KI {
     uint64_t k;  // (object << 32) | subject
     uint64_t i;  // update index << 34 | upsert << 33 | has expiration << 32 | caveat
   };
-  KI* a = reinterpret_cast<KI*>(scr.data() + n);
-  KI* b = reinterpret_cast<KI*>(scr.data() + 3 * n);
-  std::vector<uint64_t> kinds;  // distinct (relation, subject type, subject relation)
-  // (resource type, kind, wildcard subject) combinations whose schema checks passed: the checks
-  // depend on nothing else, so each is made once per batch
-  std::vector<uint64_t> seen;
-  std::vector<uint32_t> seen_g;
-  if (n >= (1ull << 30)) throw Error(GCK_E_CAPACITY, "a Watch batch holds at most 2^30 updates");
+  static_assert(sizeof(KI) == 16, "group record");
+  constexpr uint32_t kSlots = 64;
+  struct Slot {
+    uint64_t combo;
+    uint32_t kind, rows, subs, used;
+  } cache[kSlots];
+  for (Slot& sl : cache) sl.used = 0;
+  std::vector<uint64_t>& kinds = B.kinds;  // distinct (relation, subject type, subject relation)
+  kinds.clear();
+  std::vector<uint32_t>& cnt = B.cnt;
+  cnt.clear();
+  auto recs = [&](uint32_t k) -> KI* {  // the kind's record array (capacity n)
+    std::vector<uint64_t>& v = B.recs[k];
+    if (v.size() < 2 * n) v.resize(2 * n);
+    return reinterpret_cast<KI*>(v.data());
+  };
+  std::vector<KI*> arr;
+  const uint32_t n_cav = (uint32_t)std::min<size_t>(e.caveat_instances.size(), 0xFFFFFFFFu);
   for (size_t i = 0; i < n; ++i) {
     const gck_update& u = ups[i];
     if (u.op != GCK_UPDATE_CREATE && u.op != GCK_UPDATE_TOUCH && u.op != GCK_UPDATE_DELETE)
       throw Error(GCK_E_INVALID_ARGUMENT, "unknown update operation " + std::to_string(u.op));
     const gck_tuple& t = u.tuple;
+    const bool wild = t.subject_id == kWildcard;
     const uint64_t combo = ((uint64_t)(t.resource_type & 0x7FFF) << 48) | ((uint64_t)t.relation << 32) |
-                           ((uint64_t)t.subject_type << 16) | t.subject_relation |
-                           (t.subject_id == kWildcard ? (1ull << 63) : 0ull);
-    size_t c = 0;
-    while (c < seen.size() && seen[c] != combo) ++c;
-    if (c == seen.size()) {
+                           ((uint64_t)t.subject_type << 16) | t.subject_relation | (wild ? (1ull << 63) : 0ull);
+    Slot& sl = cache[(combo * 0x9E3779B97F4A7C15ull) >> 58];
+    if (sl.used && sl.combo == combo) {
+      if (t.resource_id >= sl.rows || (!wild && t.subject_id >= sl.subs) || t.caveat >= n_cav)
+        validate_tuple(e, t);  // (raises the error)
+    } else {
       validate_tuple(e, t);
       const uint64_t gk = combo & 0xFFFFFFFFFFFFull;
-      size_t j = 0;
-      while (j < kinds.size() && kinds[j] != gk) ++j;
-      if (j == kinds.size()) kinds.push_back(gk);
-      seen.push_back(combo);
-      seen_g.push_back((uint32_t)j);
-    } else if (t.resource_id >= e.interner[t.resource_type].count ||
-               (t.subject_id != kWildcard && t.subject_id >= e.interner[t.subject_type].count) ||
-               t.caveat >= e.caveat_instances.size()) {
-      validate_tuple(e, t);  // (raises the error)
+      uint32_t k = 0;
+      while (k < kinds.size() && kinds[k] != gk) ++k;
+      if (k == kinds.size()) {
+        kinds.push_back(gk);
+        cnt.push_back(0);
+        if (B.recs.size() <= k) B.recs.resize(k + 1);
+        arr.push_back(recs(k));
+      }
+      sl = Slot{combo, k, e.interner[t.resource_type].count, e.interner[t.subject_type].count, 1u};
     }
-    g_of[i] = seen_g[c];
+    const uint32_t k = sl.kind;
+    const uint64_t up = u.op != GCK_UPDATE_DELETE ? 1 : 0;
+    arr[k][cnt[k]++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
+                        ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) | t.caveat};
   }
-  (void)sc;
   pc.mark("validate");
   const size_t G = kinds.size();
-  std::vector<uint32_t> by_kind(G), rank(G);
+  std::vector<uint32_t> by_kind(G);
   for (size_t j = 0; j < G; ++j) by_kind[j] = (uint32_t)j;
   std::sort(by_kind.begin(), by_kind.end(), [&](uint32_t x, uint32_t y) { return kinds[x] < kinds[y]; });
-  for (size_t j = 0; j < G; ++j) rank[by_kind[j]] = (uint32_t)j;
-  std::vector<size_t> start(G + 1, 0);
-  for (size_t i = 0; i < n; ++i) ++start[rank[g_of[i]] + 1];
-  for (size_t j = 0; j < G; ++j) start[j + 1] += start[j];
-  {
-    std::vector<size_t> at(start.begin(), start.end() - 1);
-    // the sort records carry what the groups need (upsert, expiration present, caveat) next to
-    // the update's index, so that only updates with an expiration are read again
-    for (size_t i = 0; i < n; ++i) {
-      const gck_tuple& t = ups[i].tuple;
-      const uint64_t up = ups[i].op != GCK_UPDATE_DELETE ? 1 : 0;
-      a[at[rank[g_of[i]]]++] = {((uint64_t)t.resource_id << 32) | t.subject_id,
-                                ((uint64_t)i << 34) | (up << 33) | ((t.expires_at_us != 0 ? 1ull : 0ull) << 32) |
-                                    t.caveat};
-    }
-  }
-  pc.mark("scatter");
-  std::vector<UpdateGroup> out(G);
-  std::vector<uint32_t> cnt;
+  std::vector<UpdateGroup>& out = B.out;
+  out.resize(G);
+  if (B.tmp.size() < 2 * n) B.tmp.resize(2 * n);
+  KI* b = reinterpret_cast<KI*>(B.tmp.data());
+  std::vector<uint32_t>& bucket = B.bucket;
   for (size_t gi = 0; gi < G; ++gi) {
-    const size_t lo = start[gi], hi = start[gi + 1];
+    const uint32_t kk = by_kind[gi];
+    KI* a = arr[kk];
+    const size_t m = cnt[kk];
     // stable sort by key (a later write of a key stays after the earlier ones): one counting pass
     // on the key's top bits into ~one bucket per update, then an insertion sort of each bucket
-    // (a bucket that a skewed batch fills — many subjects of one object — is merge-sorted)
     uint64_t kmin = ~0ull, kmax = 0;
-    for (size_t i = lo; i < hi; ++i) {
+    for (size_t i = 0; i < m; ++i) {
       kmin = std::min(kmin, a[i].k);
       kmax = std::max(kmax, a[i].k);
     }
     KI* src = a;
-    const size_t m = hi - lo;
     if (m > 1 && kmax != kmin) {
       int lb = 1;
       while (lb < 16 && ((size_t)1 << lb) < m) ++lb;
       const int bits = 64 - __builtin_clzll(kmax - kmin);
       const int sh = bits > lb ? bits - lb : 0;
       const size_t nb = ((kmax - kmin) >> sh) + 1;
-      cnt.assign(nb + 1, 0u);
-      for (size_t i = lo; i < hi; ++i) ++cnt[((a[i].k - kmin) >> sh) + 1];
-      for (size_t j = 0; j < nb; ++j) cnt[j + 1] += cnt[j];
-      for (size_t i = lo; i < hi; ++i) b[lo + cnt[(a[i].k - kmin) >> sh]++] = a[i];
+      bucket.assign(nb + 1, 0u);
+      for (size_t i = 0; i < m; ++i) ++bucket[((a[i].k - kmin) >> sh) + 1];
+      for (size_t j = 0; j < nb; ++j) bucket[j + 1] += bucket[j];
+      for (size_t i = 0; i < m; ++i) b[bucket[(a[i].k - kmin) >> sh]++] = a[i];
       src = b;
-      // (cnt[j] is now the end of bucket j)
-      size_t s0 = lo;
+      // (bucket[j] is now the end of bucket j)
+      size_t s0 = 0;
       for (size_t j = 0; j < nb; ++j) {
-        const size_t s1 = lo + cnt[j];
+        const size_t s1 = bucket[j];
         if (s1 - s0 > 32) {
           std::stable_sort(b + s0, b + s1, [](const KI& x, const KI& y) { return x.k < y.k; });
         } else {
@@ -476,7 +507,7 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
         s0 = s1;
       }
     }
-    const uint64_t kind = kinds[by_kind[gi]];
+    const uint64_t kind = kinds[kk];
     UpdateGroup& g = out[gi];
     g.rel = (uint16_t)(kind >> 32);
     g.stype = (uint16_t)(kind >> 16);
@@ -487,8 +518,8 @@ std::vector<UpdateGroup> group_updates(Engine& e, const gck_update* ups, size_t 
     g.cav.resize(m);
     g.exp_us.resize(m);
     size_t w = 0;
-    for (size_t i = lo; i < hi; ++i) {
-      if (i + 1 < hi && src[i + 1].k == src[i].k) continue;  // a later write of the same relationship follows
+    for (size_t i = 0; i < m; ++i) {
+      if (i + 1 < m && src[i + 1].k == src[i].k) continue;  // a later write of the same relationship follows
       const uint64_t v = src[i].i;
       const bool up = (v >> 33) & 1, has_exp = (v >> 32) & 1;
       const uint32_t cav = (uint32_t)v;

@@ -198,6 +198,10 @@ _SIGS = {
                                       C.POINTER(C.c_size_t)]),
     "gck_set_partition": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "gck_partition_owner": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+    "gck_partition_owner_name": (C.c_uint32, [C.c_uint16, C.c_char_p, C.c_size_t, C.c_uint32]),
+    "gck_part_intern_with": (C.c_int, [_P, C.POINTER(Transport), _P, _P, _P, C.c_size_t, C.c_uint32, _P]),
+    "gck_part_add_tuples_text_with": (C.c_int, [_P, C.POINTER(Transport), C.c_char_p, C.c_size_t]),
+    "gck_interned_names": (C.c_int, [_P, C.c_uint16, C.POINTER(C.c_uint32)]),
     "gck_part_check_with": (C.c_int, [_P, C.POINTER(Transport), _P, C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_part_unique_id": (C.c_int, [_P]),
     "gck_part_init": (C.c_int, [_P, _P]),
@@ -694,6 +698,64 @@ class Engine:
         buf = (C.c_uint8 * PART_UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
         _check(self._lib.gck_part_init(self._h, buf))
 
+    def part_intern(self, transport: "Transport", type_ids, names, create: bool = False) -> np.ndarray:
+        """gck_part_intern_with (collective): the ids every rank agrees on for (type, name) pairs,
+        each interned by its owner rank (hash of the name)."""
+        n = len(names)
+        raw = [s.encode() if isinstance(s, str) else bytes(s) for s in names]
+        types = np.ascontiguousarray(type_ids, dtype=np.uint16)
+        lens = np.array([len(b) for b in raw], dtype=np.uint32)
+        bufs = [C.create_string_buffer(b, len(b) + 1) for b in raw]
+        ptrs = (C.c_char_p * max(1, n))(*[C.cast(b, C.c_char_p) for b in bufs])
+        out = np.zeros(n, dtype=np.uint32)
+        _check(self._lib.gck_part_intern_with(self._h, C.byref(transport), types.ctypes.data if n else None,
+                                              C.cast(ptrs, C.c_void_p) if n else None,
+                                              lens.ctypes.data if n else None, n, INTERN_CREATE if create else 0,
+                                              out.ctypes.data if n else None))
+        return out
+
+    def interned_names(self, type_id: int) -> int:
+        """Names the interner holds for a type (gck_interned_names)."""
+        v = C.c_uint32(0)
+        _check(self._lib.gck_interned_names(self._h, type_id, C.byref(v)))
+        return v.value
+
+    def part_add_tuples_text(self, transport: "Transport", text: str):
+        """gck_part_add_tuples_text_with (collective): the export stream's text, the same on every
+        rank; each keeps and interns what it owns."""
+        b = text.encode()
+        _check(self._lib.gck_part_add_tuples_text_with(self._h, C.byref(transport), b, len(b)))
+
+    def part_load_snapshot_text(self, transport: "Transport", revision: int, text: str):
+        self.begin_snapshot(revision)
+        self.part_add_tuples_text(transport, text)
+        self.commit_snapshot()
+
+    def part_make_items(self, transport: "Transport", rels: Iterable) -> np.ndarray:
+        """make_items on a partitioned engine (collective): the names resolved by their owners,
+        so that every rank builds the same items."""
+        rels = list(rels)
+        items = np.zeros(len(rels), dtype=ITEM_DTYPE)
+        types, names, where = [], [], []
+        for i, r in enumerate(rels):
+            rt = self.type_id(r.ResourceType)
+            st = self.type_id(r.SubjectType)
+            items[i]["resource_type"] = rt
+            items[i]["permission"] = self.relation_id(rt, r.ResourceRelation)
+            items[i]["subject_type"] = st
+            items[i]["subject_relation"] = (ELLIPSIS if r.SubjectRelation in ("", "...")
+                                            else self.relation_id(st, r.SubjectRelation))
+            items[i]["resource_id"] = ID_ABSENT
+            items[i]["subject_id"] = ID_WILDCARD if (st == TYPE_INVALID and r.SubjectID == "*") else ID_ABSENT
+            if rt != TYPE_INVALID:
+                types.append(rt), names.append(r.ResourceID), where.append((i, "resource_id"))
+            if st != TYPE_INVALID:
+                types.append(st), names.append(r.SubjectID), where.append((i, "subject_id"))
+        ids = self.part_intern(transport, types, names, create=False)
+        for (i, f), v in zip(where, ids):
+            items[i][f] = v
+        return items
+
     def part_check(self, d_items: int, n: int, d_perm: int, d_err: int, now_us: int = 0,
                    stream: Optional[int] = None):
         """gck_part_check: the whole partitioned check, exchanged over RCCL inside libgck."""
@@ -849,3 +911,9 @@ PART_UNIQUE_ID_BYTES = 128  # GCK_PART_UNIQUE_ID_BYTES
 
 def partition_owner(object_id: int, world: int) -> int:
     return load_library().gck_partition_owner(object_id, world)
+
+
+def partition_owner_name(type_id: int, name: str, world: int) -> int:
+    """The rank that owns (and interns) the named object on a partitioned graph."""
+    b = name.encode()
+    return load_library().gck_partition_owner_name(type_id, b, len(b), world)

@@ -121,6 +121,108 @@ class GlooTransport:
             return -1
 
 
+class LocalTransport:
+    """gck_transport between the ranks of one process: each rank's engine runs its collective call
+    (gck_part_intern_with, gck_part_add_tuples_text_with, gck_part_check_with) on its own thread,
+    and the blocks meet in host memory behind a barrier per collective. For rehearsals and tests
+    of several ranks' engines in one process (one GPU or several); ``endpoint(rank).c`` is the
+    struct a rank passes."""
+
+    class _End:
+        def __init__(self, hub, rank):
+            self.hub, self.rank = hub, rank
+            self.error: Optional[str] = None
+            self._a2a = ALLTOALLV_FN(self._alltoallv)
+            self._ar = ALLREDUCE_MAX_U8_FN(self._allreduce)
+            self.c = Transport(None, self._a2a, self._ar)
+
+        def _get(self, src, n, stream):
+            buf = (ctypes.c_uint8 * max(1, n))()
+            if n:
+                rc = _hip().hipMemcpyAsync(ctypes.addressof(buf), src, n, 4, stream)
+                if rc != 0 or _hip().hipStreamSynchronize(stream) != 0:
+                    raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+            return bytes(buf)[:n]
+
+        def _put(self, dst, data, stream):
+            if data:
+                src = ctypes.create_string_buffer(data, len(data))
+                rc = _hip().hipMemcpyAsync(dst, ctypes.addressof(src), len(data), 4, stream)
+                if rc != 0 or _hip().hipStreamSynchronize(stream) != 0:
+                    raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+        def _alltoallv(self, ctx, send, send_bytes, recv, recv_bytes, stream) -> int:
+            try:
+                h, w = self.hub, self.hub.world
+                _hip().hipStreamSynchronize(stream)
+                sb = [int(send_bytes[i]) for i in range(w)]
+                rb = [int(recv_bytes[i]) for i in range(w)]
+                flat = self._get(send, sum(sb), stream)
+                blocks, at = [], 0
+                for k in range(w):
+                    blocks.append(flat[at:at + sb[k]])
+                    at += sb[k]
+                h.box[self.rank] = blocks
+                h.barrier.wait()
+                got = b"".join(h.box[s][self.rank] for s in range(w))
+                h.barrier.wait()
+                if len(got) != sum(rb):
+                    raise RuntimeError(f"alltoallv: {len(got)} bytes arrived, {sum(rb)} expected")
+                self._put(recv, got, stream)
+                return 0
+            except Exception:  # (an exception may not cross the C ABI)
+                self.error = self.error or traceback.format_exc()
+                self.hub.barrier.abort()
+                return -1
+
+        def _allreduce(self, ctx, buf, n, stream) -> int:
+            try:
+                h = self.hub
+                _hip().hipStreamSynchronize(stream)
+                h.box[self.rank] = self._get(buf, int(n), stream)
+                h.barrier.wait()
+                out = bytes(max(col) for col in zip(*h.box)) if n else b""
+                h.barrier.wait()
+                self._put(buf, out, stream)
+                return 0
+            except Exception:
+                self.error = self.error or traceback.format_exc()
+                self.hub.barrier.abort()
+                return -1
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.box = [None] * world
+        self.ends = [LocalTransport._End(self, r) for r in range(world)]
+
+    def endpoint(self, rank: int) -> "LocalTransport._End":
+        return self.ends[rank]
+
+    def run(self, fn):
+        """fn(rank) on one thread per rank, together (a collective of every rank); the first
+        exception is raised here."""
+        import threading
+        errs = [None] * self.world
+
+        def body(r):
+            try:
+                fn(r)
+            except BaseException as ex:  # noqa: BLE001
+                errs[r] = ex
+                self.barrier.abort()
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(self.world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        self.barrier.reset()
+        for ex in errs:
+            if ex is not None:
+                raise ex
+
+
 class PartitionedChecker:
     """Checks batches on a partitioned engine (``Engine.set_partition`` before the snapshot) over
     a torch.distributed group: every rank of ``group`` calls :meth:`check` with the same items and

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 10
+#define GCK_ABI_VERSION 11
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -421,6 +421,30 @@ typedef struct gck_transport {
                    const uint64_t* recv_bytes, void* stream);
   int (*allreduce_max_u8)(void* ctx, void* d_buf, uint64_t n, void* stream);
 } gck_transport;
+
+/* Object names on a partitioned engine (world > 1; SURVEY.md §8e: owner = hash(type, id) mod G).
+ * A name's owner is gck_partition_owner_name(type, name) — FNV-1a over the type (2 bytes, little
+ * endian) and the name's bytes, finalised, mod world — decided before anything is interned, and
+ * only the owner gives it an id: local * world + owner, in the order the owner meets its names, so
+ * that gck_partition_owner(id) is the same rank and every rank holds the same id for a name. A rank
+ * keeps only the names of what it owns and of what its rows and checks reference (the replicated
+ * hub hierarchy among them); local interning of a new name (gck_intern with GCK_INTERN_CREATE,
+ * gck_add_tuples_text, gck_apply_updates_text) is refused with GCK_E_STATE on such an engine.
+ * Both calls below are collective: every rank of the partition calls them, in the same order. */
+uint32_t gck_partition_owner_name(uint16_t type, const char* name, size_t len, uint32_t world);
+/* Every rank its own names (types[i], names[i] of lens[i] bytes) -> out_ids[i]: "*" is
+ * GCK_ID_WILDCARD; a name the owner does not know is created with GCK_INTERN_CREATE, else
+ * GCK_ID_ABSENT (check items: build them with this, so that every rank has the same items). With
+ * GCK_INTERN_CREATE every rank's object counts become world x the largest owner's count. */
+int gck_part_intern_with(gck_engine* e, const gck_transport* t, const uint16_t* types, const char* const* names,
+                         const uint32_t* lens, size_t n, uint32_t flags, uint32_t* out_ids);
+/* The export stream's relationships as text (gck_add_tuples_text's format), the same text on every
+ * rank, between gck_begin_snapshot and gck_commit_snapshot: each rank keeps what it owns (decided
+ * from the names) and interns the names of those relationships only, through their owners. */
+int gck_part_add_tuples_text_with(gck_engine* e, const gck_transport* t, const char* text, size_t len);
+/* The names this engine's interner holds for a type (on a partitioned engine: its own objects'
+ * and those its rows and checks referenced; otherwise every named object). */
+int gck_interned_names(gck_engine* e, uint16_t type, uint32_t* out);
 
 /* The partitioned check over the caller's transport: n device items (the same on every rank) in,
  * every result out on every rank (d_out_perm / d_out_err, device). `now_us` 0 = rank 0's clock. */

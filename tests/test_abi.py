@@ -45,7 +45,7 @@ def test_struct_layouts_match_header():
     assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
     assert C.sizeof(E._Stats) == 232
-    assert E.load_library().gck_abi_version() == 10
+    assert E.load_library().gck_abi_version() == 11
 
 
 @pytest.fixture()

@@ -24,7 +24,7 @@ KERNELS = {
     "void gck::k_label_join<24, 32u, 32u, true>(gck::LjArgs)": [160],
     "void gck::k_label_join<32, 16u, 32u, true>(gck::LjArgs)": [160],
     "void gck::k_label_join<32, 32u, 32u, true>(gck::LjArgs)": [160],
-    "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [336, 144],
+    "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [344, 144],
 }
 
 

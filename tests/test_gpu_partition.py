@@ -32,14 +32,23 @@ def _free_port():
     return port
 
 
-def _family_engine(rank, world, family, seed):
+def _family_engine(rank, world, family, seed, transport):
+    # the export stream as text on every rank: each keeps and interns what it owns (names owned by
+    # hash, interned by their owner: gck_part_add_tuples_text_with), and the check items are built
+    # through the owners too, so every rank holds the same items
     schema, tuples, checks = gen.FAMILIES[family](seed)
     e = E.Engine(device=0, max_depth=gen.FAMILY_DEPTH.get(family, 50))
     e.set_partition(rank, world)
     e.load_schema(schema)
-    e.load_snapshot_text(1, "\n".join(tuples))
-    items = e.make_items([parse_check(c) for c in checks])
+    e.part_load_snapshot_text(transport.c, 1, "\n".join(tuples))
+    items = e.part_make_items(transport.c, [parse_check(c) for c in checks])
     return e, torch.from_numpy(items.view(np.uint8).copy()).cuda(), len(items)
+
+
+def _names_held(e):
+    n_types = E.C.c_uint32(0)
+    e._lib.gck_type_count(e._h, E.C.byref(n_types))
+    return sum(e.interned_names(t) for t in range(n_types.value))
 
 
 def _synth_engine(rank, world, tuples):
@@ -84,7 +93,10 @@ def _worker(rank, world, port, family, seed, out_dir, watch):
                 e.apply_updates(2, C.batch(max(1000, int(G.n_tuples * 0.001)), cycle=False))
                 res["revision"] = e.revision
         else:
-            e, d_items, n = _family_engine(rank, world, family, seed)
+            from gochugaru_amd.partition import GlooTransport
+            tr = GlooTransport(None, device=True)
+            e, d_items, n = _family_engine(rank, world, family, seed, tr)
+            res["names"] = _names_held(e)
             pc = PartitionedChecker(e)
         e.reset_stats()
         perm, err = pc.check(d_items, n, now_us=gen.NOW_US)
@@ -131,6 +143,17 @@ def test_partitioned_matches_oracle(tmp_path, world, family, seed):
     assert not bad, bad[:5]
     total = len(set(tuples))
     assert all(o["tuples"] < total for o in outs), [o["tuples"] for o in outs]
+    # names interned by their owners only: no rank holds every object's name
+    rep = E.Engine(device=0)
+    rep.load_schema(schema)
+    rep.load_snapshot_text(1, "\n".join(tuples))
+    all_names = _names_held(rep)
+    rep.close()
+    # (names are interned by their owners; on these small dense graphs a rank's rows still reference
+    # nearly every object: test_partitioned_ranks_intern_their_own_names measures the fraction)
+    assert all(o["names"] <= all_names for o in outs), ([o["names"] for o in outs], all_names)
+    print(json.dumps({"family": family, "world": world, "names_held": [o["names"] for o in outs],
+                      "replicated_names": all_names}))
     if family == "github":  # the term conjunction (exclusion, intersection) partitions too
         assert outs[0]["label_checks"] > 0
 
@@ -244,14 +267,16 @@ def test_invalid_update_rejected_on_every_rank():
     rank refuses the whole batch and stays at the old revision (each validates the batch before
     it keeps its own updates, gck_api.cpp apply_updates), so no rank moves ahead of the others.
     The engines of both ranks live in this process: applying a batch needs no exchange."""
+    from gochugaru_amd.partition import LocalTransport
     schema, tuples, _ = gen.FAMILIES["gdocs"](2)
     engines = []
     for r in range(2):
         e = E.Engine(device=0)
         e.set_partition(r, 2)
         e.load_schema(schema)
-        e.load_snapshot_text(1, "\n".join(tuples))
         engines.append(e)
+    lt = LocalTransport(2)  # (both ranks' engines in this process, one thread each)
+    lt.run(lambda r: engines[r].part_load_snapshot_text(lt.endpoint(r).c, 1, "\n".join(tuples)))
     e0 = engines[0]
     t_doc, t_user, t_folder = e0.type_id("doc"), e0.type_id("user"), e0.type_id("folder")
     viewer = e0.relation_id(t_doc, "viewer")
@@ -279,3 +304,100 @@ def test_invalid_update_rejected_on_every_rank():
         assert e.revision == 2
     for e in engines:
         e.close()
+
+
+def _named_config4(seed=5, n_users=20000, n_groups=800, layers=8, n_docs=3000):
+    """The config-4 shape with names (users dominate, a layered group DAG, documents granting
+    groups), as text: what a partitioned engine reads from the export stream."""
+    import random
+    rng = random.Random(seed)
+    t, per = [], n_groups // layers
+    members, viewers = {}, {}
+    for g in range(n_groups):
+        layer = g // per
+        for _ in range(rng.randint(0, 60)):
+            u = rng.randrange(n_users)
+            members.setdefault(g, []).append(u)
+            t.append(f"group:g{g}#member@user:u{u}")
+        if layer + 1 < layers:
+            for _ in range(rng.randint(0, 3)):
+                t.append(f"group:g{g}#member@group:g{(layer + 1) * per + rng.randrange(per)}#member")
+    for d in range(n_docs):
+        for _ in range(rng.randint(1, 3)):
+            g = rng.randrange(n_groups)
+            viewers.setdefault(d, []).append(g)
+            t.append(f"doc:d{d}#viewer@group:g{g}#member")
+    checks = [f"doc:d{rng.randrange(n_docs)}#view@user:u{rng.randrange(n_users)}" for _ in range(1200)]
+    for _ in range(300):  # (positives: a direct member of one of the document's groups)
+        d = rng.randrange(n_docs)
+        g = rng.choice(viewers[d])
+        if members.get(g):
+            checks.append(f"doc:d{d}#view@user:u{rng.choice(members[g])}")
+    checks += [f"group:g{rng.randrange(n_groups)}#member@user:u{rng.randrange(n_users)}" for _ in range(200)]
+    checks += [f"doc:d{rng.randrange(n_docs)}#view@group:g{rng.randrange(n_groups)}#member" for _ in range(100)]
+    checks += [f"doc:d{rng.randrange(n_docs + 50)}#view@user:u{rng.randrange(n_users + 500)}" for _ in range(100)]
+    return gen.NESTED, sorted(set(t)), checks
+
+
+def _named_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from gochugaru_amd.partition import GlooTransport, PartitionedChecker
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        schema, tuples, checks = _named_config4()
+        tr = GlooTransport(None, device=True)
+        e, d_items, n = _family_engine_named(rank, world, schema, tuples, checks, tr)
+        pc = PartitionedChecker(e)
+        e.reset_stats()
+        perm, err = pc.check(d_items, n, now_us=gen.NOW_US)
+        st = e.stats()
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump({"perm": perm.cpu().tolist(), "err": err.cpu().tolist(), "names": _names_held(e),
+                       "tuples": e.tuple_count, "label_checks": int(st["label_checks"]), "n": n}, f)
+        e.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _family_engine_named(rank, world, schema, tuples, checks, transport):
+    e = E.Engine(device=0)
+    e.set_partition(rank, world)
+    e.load_schema(schema)
+    e.part_load_snapshot_text(transport.c, 1, "\n".join(tuples))
+    items = e.part_make_items(transport.c, [parse_check(c) for c in checks])
+    return e, torch.from_numpy(items.view(np.uint8).copy()).cuda(), len(items)
+
+
+def test_partitioned_ranks_intern_their_own_names(tmp_path):
+    """Ownership decided before interning (owner = hash(type, name) mod G): the
+    config-4 shape read as text by 2 ranks, each keeping its own rows — a group's direct members
+    with the members' owner, the hierarchy everywhere — and interning the names of those tuples
+    only, through their owners. Each rank's interner holds at most 0.6x the objects the
+    replicated engine interns, and every check is bit-exact against the oracle."""
+    import torch.multiprocessing as mp
+    mp.spawn(_named_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
+    assert outs[0]["perm"] == outs[1]["perm"] and outs[0]["err"] == outs[1]["err"]
+    schema, tuples, checks = _named_config4()
+    rep = E.Engine(device=0)
+    rep.load_schema(schema)
+    rep.load_snapshot_text(1, "\n".join(tuples))
+    all_names = _names_held(rep)
+    rep.close()
+    ck = oracle_for(schema, tuples, now=gen.NOW_US / 1e6)
+    want = [ck.check(to_oracle_item(parse_check(c))) for c in checks]
+    got = list(zip(outs[0]["perm"], outs[0]["err"]))
+    bad = [(c, w, g) for c, w, g in zip(checks, want, got) if tuple(w) != tuple(g)]
+    assert not bad, bad[:5]
+    assert sum(1 for p, _ in got if p == E.PERM_HAS) > 200
+    print(json.dumps({"names_held": [o["names"] for o in outs], "replicated_names": all_names,
+                      "tuples": [o["tuples"] for o in outs], "all_tuples": len(tuples),
+                      "label_checks": [o["label_checks"] for o in outs], "n": outs[0]["n"]}))
+    for o in outs:
+        assert o["names"] <= 0.6 * all_names, (o["names"], all_names)
+        assert o["tuples"] <= 0.6 * len(tuples), (o["tuples"], len(tuples))

@@ -73,3 +73,30 @@ def test_owner_matches_library():
     for world in (1, 2, 3, 8):
         for obj in list(range(0, 2000, 7)) + [2**31, 2**32 - 3]:
             assert E.partition_owner(obj, world) == (0 if world == 1 else obj % world)
+
+
+def _owner_name(type_id: int, name: str, world: int) -> int:
+    """The name's owner restated (include/gck.h gck_partition_owner_name): FNV-1a 64 over the type
+    id (2 bytes, little endian) and the name's bytes, a murmur-style finaliser, mod world."""
+    m = (1 << 64) - 1
+    h = 1469598103934665603
+    for b in bytes([type_id & 0xFF, type_id >> 8]) + name.encode():
+        h = ((h ^ b) * 1099511628211) & m
+    h ^= h >> 33
+    h = (h * 0xff51afd7ed558ccd) & m
+    h ^= h >> 33
+    return h % world if world > 1 else 0
+
+
+def test_owner_of_a_name_matches_library():
+    """Ownership by name (hash(type, id) mod G), decided before any interning: the
+    library's function equals its restatement, and spreads names evenly over the ranks."""
+    lib = E.load_library()
+    names = [f"user{k}" for k in range(4000)] + ["", "*", "doc:x", "üñí", "a" * 300]
+    for world in (1, 2, 3, 8):
+        for t in (0, 1, 7, 300):
+            for nm in names[:50] + names[-5:]:
+                b = nm.encode()
+                assert lib.gck_partition_owner_name(t, b, len(b), world) == _owner_name(t, nm, world), (t, nm, world)
+        counts = np.bincount([E.partition_owner_name(2, nm, world) for nm in names[:4000]], minlength=world)
+        assert counts.min() > 0.8 * 4000 / world, counts

@@ -11,6 +11,14 @@
 #   bash tools/gpu.sh phases <tag> [bench args]          bench with GCK_DEBUG_PHASES=1 (snapshot / Watch
 #                                                        phase times on stderr)
 #   bash tools/gpu.sh pmcprobe <tag> [bench args]        one FETCH_SIZE pass over the AQL path (GCK_DEBUG_AQL)
+#   bash tools/gpu.sh final <tag>                        the round-end set: pytest -m gpu, smoke, the
+#                                                        driver-sized headline (twice), 2000 steps, config 5
+#                                                        (20 and 500 steps), and the headline's kernel trace
+#   bash tools/gpu.sh mixed <tag> [bench args]           config 5 with the Watch phases (GCK_DEBUG_PHASES)
+#   bash tools/gpu.sh probes <tag>                       host-link placement (tools/pcie_probe), the
+#                                                        host-batch timeline (tools/host_probe.py), the
+#                                                        Watch grouping (tools/group_bench), the AQL span
+#                                                        attribution (tools/aql_span.sh)
 set -e
 CMD=$1
 TAG=$2
@@ -83,8 +91,39 @@ case "$CMD" in
     find "$OUT" -name "*agent_info.csv" -delete
     exit $rc
     ;;
+  final)
+    set +e
+    timeout -k 10 700 python -u -m pytest -m gpu -q -rf --timeout 300 --timeout-method thread tests/ > "$OUT/pytest.log" 2>&1
+    rc=$?
+    echo "pytest rc=$rc" >> "$OUT/pytest.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+    set -e
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1
+    for r in 1 2; do
+      timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_driver$r.json" 2> "$OUT/bench_driver$r.err"
+    done
+    timeout -k 10 300 python3 bench.py --no-cpu > "$OUT/bench_2000.json" 2> "$OUT/bench_2000.err"
+    timeout -k 10 300 python3 bench.py --config mixed --steps 20 --warmup 5 > "$OUT/mixed20.json" 2> "$OUT/mixed20.err"
+    timeout -k 10 400 python3 bench.py --config mixed --steps 500 --no-cpu > "$OUT/mixed500.json" 2> "$OUT/mixed500.err"
+    GCK_AQL_TIMED=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/kt.json" 2> "$OUT/kt.err"
+    find "$OUT" -name "*kernel_trace.csv" -delete
+    find "$OUT" -name "*agent_info.csv" -delete
+    tail -2 "$OUT/pytest.log"
+    ;;
+  mixed)
+    GCK_DEBUG_PHASES=1 timeout -k 10 400 python3 bench.py --config mixed "$@" > "$OUT/mixed.json" 2> "$OUT/mixed.err" \
+      || { tail -20 "$OUT/mixed.err"; exit 1; }
+    grep "gck watch\]\|gck apply\]\|gck relink\|gck group\|apply_publish" "$OUT/mixed.err" | tail -5
+    ;;
+  probes)
+    timeout -k 10 120 tools/pcie_probe/pcie_probe > "$OUT/pcie_probe.jsonl" 2> "$OUT/pcie_probe.err"
+    timeout -k 10 200 python3 tools/host_probe.py > "$OUT/host_probe.json" 2> "$OUT/host_probe.err"
+    timeout -k 10 120 tools/group_bench/group_bench 9844 400 > "$OUT/group_bench.json"
+    bash tools/aql_span.sh "$OUT/aql_span"
+    ;;
   *)
-    echo "usage: tools/gpu.sh tests|bench|sweep|profile|phases <tag> [args]" >&2
+    echo "usage: tools/gpu.sh tests|bench|sweep|profile|phases|pmcprobe|final|mixed|probes <tag> [args]" >&2
     exit 2
     ;;
 esac
