@@ -99,6 +99,9 @@ def parse():
                          "config 5 with 32K per-relationship caveat contexts x one context per request")
     ap.add_argument("--selftest", action="store_true", help="launcher / rank bookkeeping only (no GPU; tests)")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
+    ap.add_argument("--watch-stage", type=int, default=1,
+                    help="config 5: stage the next step's Watch batch (gck_watch_stage: grouped on the engine's "
+                         "thread) while the step applies its own; 0 = gck_apply_updates")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     args = ap.parse_args()
     nested = args.config == "nested"
@@ -434,13 +437,26 @@ def main():
         from gochugaru_amd.engine import Contexts
         n_up = max(1, int(n_tuples * args.churn))
         batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warm + args.steps)]
-        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "pending": None}
+        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "pending": None, "ticket": None}
         m_ctx = Contexts(CONTEXTS)
 
         def step():
             t_a = time.perf_counter()
             rev["r"] += 1
-            eng.apply_updates(rev["r"], batches[rev["k"]])
+            k = rev["k"]
+            if args.watch_stage:
+                # a Watch consumer holding the next batch stages it (the engine's thread validates
+                # and groups it) before it applies this one: every step still groups, merges and
+                # publishes one whole batch, the next batch's grouping beside this one's merge
+                if rev["ticket"] is None:
+                    rev["ticket"] = eng.stage_updates(batches[k])
+                # (the last step stages its own batch again, discarded after the run: every timed
+                # step stages one batch, so the timed region holds as many groupings as applies)
+                nxt = eng.stage_updates(batches[min(k + 1, len(batches) - 1)])
+                eng.apply_staged(rev["r"], rev["ticket"])
+                rev["ticket"] = nxt
+            else:
+                eng.apply_updates(rev["r"], batches[k])
             rev["k"] += 1
             rev["apply_s"] += time.perf_counter() - t_a
             t_s = time.perf_counter()
@@ -459,6 +475,9 @@ def main():
             if rev["pending"] is not None:
                 rev["pending"].wait()
                 rev["pending"] = None
+            if rev["ticket"] is not None and rev["k"] >= len(batches):
+                eng.discard_staged(rev["ticket"])
+                rev["ticket"] = None
     elif WL.kind == "quota":
         # per step one batch with its own 64K contexts (pre-generated, rotated): the contexts are
         # parsed, the walk records the (instance, context) pairs it meets, the host evaluates
@@ -1107,7 +1126,13 @@ def main():
                           "share_of_step": round(rev["apply_timed"] / elapsed, 3),
                           "check_submit_ms_per_step": round(rev["submit_timed"] / args.steps * 1e3, 3),
                           "check_wait_ms_per_step": round(rev["wait_timed"] / args.steps * 1e3, 3),
-                          "revision": rev["r"]}} if WL.kind == "mixed" else {}),
+                          "revision": rev["r"],
+                          "staged": bool(args.watch_stage),
+                          "staging": ("gck_watch_stage: each step stages the next Watch batch (validated and grouped "
+                                      "on the engine's thread) and then applies its own (gck_watch_apply_staged: "
+                                      "merge, re-link, publication); the grouping of step k+1 runs beside step k's "
+                                      "device work" if args.watch_stage else "gck_apply_updates: grouping inside the "
+                                      "apply")}} if WL.kind == "mixed" else {}),
             **({"check_stage": check_stage} if check_stage else {}),
         }
         print(json.dumps(line), flush=True)

@@ -523,6 +523,18 @@ __device__ __forceinline__ void store_result(T* p, T v, bool coherent) {
   else
     *gptr_w(p) = v;
 }
+// A join's `coherent` word: kPubCoherent = results written through the L2 (above);
+// kPubBySignal = the batch was dispatched into an engine HSA queue (aql.inc), whose packet's
+// system-scope release fence and completion signal the host waits on: the last block's sequence
+// word then needs no release of its own (a release there writes the L2s back mid-kernel, once
+// more before the packet's own write-back, and waits for it: the dispatch span's tail)
+constexpr uint32_t kPubCoherent = 1u, kPubBySignal = 2u;
+__device__ __forceinline__ void pub_seq_store(unsigned* p, unsigned seq, uint32_t coherent) {
+  if (coherent & kPubBySignal)
+    __hip_atomic_store(p, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __hip_atomic_store(p, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint32_t csr_off(const DevCSR& r, uint32_t i) { return gptr(r.off)[i]; }
 __device__ __forceinline__ uint32_t csr_nbr(const DevCSR& r, uint32_t p) { return gptr(r.nbr)[p]; }
 __device__ __forceinline__ uint32_t csr_cav(const DevCSR& r, uint32_t p) { return gptr(r.cav)[p]; }
@@ -1285,6 +1297,24 @@ static uint32_t ceil_log2(uint64_t x) {
   return b;
 }
 
+// Waits for `ev` by polling its status. hipEventSynchronize / hipStreamSynchronize wait actively
+// only briefly and then sleep until the completion interrupt: a Watch batch's waits of a few
+// dozen microseconds then pay the wake-up on top (config 5: the merge totals, the merged CSRs,
+// the index patch). The host thread applying a Watch batch has nothing else to do meanwhile.
+static void spin_event(hipEvent_t ev) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(ev);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) HIP_OK(r);
+    __builtin_ia32_pause();
+  }
+}
+// everything enqueued on `s` so far has completed (the engine's Watch event; one writer at a time)
+static void spin_stream(Engine& e, hipStream_t s) {
+  HIP_OK(hipEventRecord((hipEvent_t)e.sync_ev, s));
+  spin_event((hipEvent_t)e.sync_ev);
+}
+
 template <class T>
 static T* dalloc(std::vector<void*>& list, size_t count, uint64_t* bytes = nullptr) {
   void* p = nullptr;
@@ -1387,6 +1417,9 @@ int device_init(Engine& e) {
   hipEvent_t dev = nullptr;
   HIP_OK(hipEventCreateWithFlags(&dev, hipEventDisableTiming));
   e.delta_ev = dev;
+  hipEvent_t sev = nullptr;
+  HIP_OK(hipEventCreateWithFlags(&sev, hipEventDisableTiming));
+  e.sync_ev = sev;
   e.device_ready = true;
   return 0;
 }
@@ -1485,6 +1518,11 @@ void device_free(Engine& e) {
     e.free_stream = nullptr;
     if (e.delta_ev) (void)hipEventDestroy((hipEvent_t)e.delta_ev);
     e.delta_ev = nullptr;
+    if (e.sync_ev) (void)hipEventDestroy((hipEvent_t)e.sync_ev);
+    e.sync_ev = nullptr;
+    if (e.blob_host) (void)hipHostFree(e.blob_host);
+    e.blob_host = nullptr;
+    e.blob_host_cap = 0;
     e.device_ready = false;
   }
 }
@@ -1668,7 +1706,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
     // only — a device-wide synchronisation would also wait for the check batches running on the
     // engine's non-blocking streams beside the build (config 5: ~55 us of a 0.29 ms Watch batch)
     pc.mark("csr_loop");
-    if (delta) HIP_OK(hipStreamSynchronize(nullptr));
+    if (delta) spin_stream(e, nullptr);
     else HIP_OK(hipDeviceSynchronize());
     pc.mark("csr_sync");
     // link the node program to the CSR table
@@ -1729,7 +1767,21 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
     for (size_t n = 0; n < hp.size(); ++n) hp[n] = (unsigned long long)(uintptr_t)ds->hgt[n];
     const size_t o_hgt = put(hp.data(), hp.size() * 8);
     unsigned char* d_blob = dalloc<unsigned char>(ds->allocs, blob.size(), &ds->bytes);
-    HIP_OK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    if (delta) {
+      // a Watch batch: from the engine's pinned blob buffer, on the null stream; complete before
+      // the snapshot is published (device_apply_publish waits for the null stream)
+      if (e.blob_host_cap < blob.size()) {
+        if (e.blob_host) HIP_OK(hipHostFree(e.blob_host));
+        e.blob_host = nullptr;
+        e.blob_host_cap = 0;
+        HIP_OK(hipHostMalloc(&e.blob_host, blob.size() * 2, hipHostMallocDefault));
+        e.blob_host_cap = blob.size() * 2;
+      }
+      std::memcpy(e.blob_host, blob.data(), blob.size());
+      HIP_OK(hipMemcpyAsync(d_blob, e.blob_host, blob.size(), hipMemcpyHostToDevice, nullptr));
+    } else {
+      HIP_OK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    }
     ds->nodes = reinterpret_cast<DevNode*>(d_blob + o_nodes);
     ds->items = reinterpret_cast<DevItem*>(d_blob + o_items);
     ds->csrs = reinterpret_cast<DevCSR*>(d_blob + o_csrs);
@@ -1763,7 +1815,7 @@ static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& ad
       if (sp.n)
         hipLaunchKernelGGL(k_slot_scatter, dim3(grid_for(sp.n)), dim3(kBlock), 0, 0, sp.slots, sp.staged, sp.ids, sp.n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(nullptr));
+    spin_stream(e, nullptr);
     ds->slot_patches.clear();
     pc.mark("slot_patch");
   }
@@ -2420,6 +2472,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.cx = w.d_ctx;
     }
     if (ak) {
+      if (j.h_out) j.coherent |= kPubBySignal;
       aql_dispatch(*e.aql, w, *ak, &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves), w.b_timed,
                    cav ? &c : nullptr, cav ? sizeof(Ctx) : 0);
       w.b_aql = true;
@@ -2474,6 +2527,8 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     } cj_args{c, j};  // (the kernarg segment: the two by-value parameters in order)
     static_assert(offsetof(decltype(cj_args), j) == 344, "k_closure_join kernarg layout (Ctx, CjArgs)");
     // (half slots: the first 32 B of each resource slot, closure.inc HALF)
+    if (fast && aql_ok && j.h_out && aql_kernel(e.aql, "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)"))
+      cj_args.j.coherent |= kPubBySignal;
     if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
                         sizeof(cj_args), grid.x)) {
     } else if (fast)

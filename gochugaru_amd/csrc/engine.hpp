@@ -217,10 +217,17 @@ struct Engine {
   void* delta_scratch = nullptr;  // device arena of Watch-batch application (delta.inc)
   void* free_stream = nullptr;    // hipStream_t: replaced snapshot arrays go back to the pool here
   void* delta_ev = nullptr;       // hipEvent_t: a Watch batch's merge totals are back (delta.inc)
+  void* sync_ev = nullptr;        // hipEvent_t: the Watch path's polled waits (engine.hip spin_stream)
+  void* blob_host = nullptr;      // pinned: a Watch batch's program upload (device_build)
+  size_t blob_host_cap = 0;
   size_t delta_scratch_cap = 0;
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
   GroupBuffers group_buf;  // group_updates' records and groups, kept across Watch batches
+  // bumped by every write that can invalidate a batch validated earlier (a schema, a snapshot file,
+  // an interner rollback, a partition): a staged Watch batch (gck_watch_stage) is regrouped at
+  // apply time when it moved
+  uint64_t shape_gen = 0;
   // merged-CSR arrays of retired snapshots kept for the next Watch batch's merge (engine.hip
   // ralloc / retire_array): bytes -> array, and every array ralloc handed out -> its bytes
   std::multimap<size_t, void*> recycle;
@@ -283,7 +290,13 @@ void load_snapshot_file(Engine& e, const std::string& path);
 std::vector<HostCSR> build_csrs(Engine& e);
 // Watch updates (rel.Update, rel/relationship.go:267-301): text lines "<OP> <relationship>"
 void parse_updates_text(Engine& e, const char* text, size_t len, std::vector<gck_update>& out);
-const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, size_t n);
+// `schema_mu`: held shared around each read of the schema and the interner (a batch staged on
+// another thread, gck_watch_stage); null when the caller holds the engine lock
+const std::vector<UpdateGroup>& group_updates(const Engine& e, GroupBuffers& B, const gck_update* ups, size_t n,
+                                              std::shared_mutex* schema_mu = nullptr);
+inline const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, size_t n) {
+  return group_updates(e, e.group_buf, ups, n);
+}
 void validate_updates(const Engine& e, const gck_update* ups, size_t n);
 
 // engine.hip

@@ -1,8 +1,10 @@
 // gck_api.cpp — the extern "C" boundary (include/gck.h). Every entry point converts C++
 // exceptions into a negative status plus a thread-local message (gck_last_error).
+#include <condition_variable>
 #include <cstring>
 #include <string>
 #include <string_view>
+#include <thread>
 
 #include "engine.hpp"
 
@@ -21,6 +23,7 @@ Engine::~Engine() {
 }
 
 void reset_caveats(Engine& e) {
+  ++e.shape_gen;  // (with the schema and a snapshot file: the interner starts over too)
   e.caveat_instances.assign(1, {"", ""});
   e.caveat_ids.clear();
   e.caveat_expr.assign(1, nullptr);
@@ -127,8 +130,44 @@ void stage_tuples(Engine& e, const gck_tuple* t, size_t n);
 
 using namespace gck;
 
+// Watch batches staged ahead of their apply (gck_watch_stage): an engine-owned thread validates
+// and groups batch k + 1 while batch k applies — a Watch consumer (client/client.go:370-413)
+// receives the next batch while it applies the previous one. Each staged batch has its own
+// grouping buffers; kSlots may be staged at once. The stager reads the schema and the interner
+// under the engine lock held shared and briefly (group_updates' schema_mu), and records the
+// engine's shape generation: a batch staged before a write that moved it is regrouped at apply.
+struct WatchStager {
+  static constexpr int kSlots = 4;
+  struct Slot {
+    const gck_update* ups = nullptr;
+    size_t n = 0;
+    uint64_t ticket = 0;  // 0: free
+    int state = 0;        // 1 queued, 2 grouped (or failed)
+    bool ok = false;
+    uint64_t gen = 0;
+    std::vector<gck_update> mine;  // (a partitioned rank's own updates)
+    GroupBuffers buf;
+    const std::vector<UpdateGroup>* groups = nullptr;
+  } slots[kSlots];
+  std::mutex m;
+  std::condition_variable cv_job, cv_done;
+  std::thread th;
+  bool stop = false;
+  uint64_t next_ticket = 1;
+  ~WatchStager() {
+    if (!th.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv_job.notify_all();
+    th.join();
+  }
+};
+
 struct gck_engine {
   Engine impl;
+  WatchStager stage;  // (destroyed first: its thread ends before the engine does)
 };
 
 template <class F>
@@ -526,15 +565,16 @@ int gck_device_bytes(gck_engine* ge, uint64_t* out) {
 // snapshot; it is taken exclusively again only to finish the batches in flight, patch the
 // membership indexes and swap the snapshot in (device_apply_publish). `lk` (exclusive, with
 // writer_mu held) is released and re-acquired here. A device failure loses the snapshot.
+// `staged`: the batch's groups, made ahead by the stager (gck_watch_apply_staged)
 static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, uint64_t revision, const gck_update* ups,
-                          size_t n) {
+                          size_t n, const std::vector<UpdateGroup>* staged = nullptr) {
   REQUIRE(e.committed, GCK_E_STATE, "no snapshot committed");
   REQUIRE(revision > e.revision || (n == 0 && revision == e.revision), GCK_E_REVISION,
           "update revision " + std::to_string(revision) + " is not newer than the snapshot's " +
               std::to_string(e.revision));
   PhaseClock pc("watch");
   std::vector<gck_update> mine;
-  if (e.part_world > 1) {  // partitioned graph: the updates of what this rank keeps (part_keep)
+  if (e.part_world > 1 && !staged) {  // partitioned graph: the updates of what this rank keeps (part_keep)
     // the whole batch validated first, as every rank validates it: an update another rank would
     // keep and reject fails the batch here too (every rank stays at the old revision)
     validate_updates(e, ups, n);
@@ -552,7 +592,8 @@ static void apply_updates(Engine& e, std::unique_lock<std::shared_mutex>& lk, ui
   bool built = false;
   try {
     std::shared_lock<std::shared_mutex> sl(e.mu);  // (checks run on the current snapshot meanwhile)
-    const std::vector<UpdateGroup>& groups = group_updates(e, ups, n);  // (the engine's, until the next batch)
+    // (the engine's, until the next batch; or the staged batch's)
+    const std::vector<UpdateGroup>& groups = staged ? *staged : group_updates(e, ups, n);
     pc.mark("group");
     if (!groups.empty()) device_apply_build(e, groups, wb);
     built = true;
@@ -593,6 +634,129 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
   });
 }
 
+// The stager's thread: groups the queued batches in ticket order.
+static void stager_loop(gck_engine* ge) {
+  Engine& e = ge->impl;
+  WatchStager& st = ge->stage;
+  std::unique_lock<std::mutex> g(st.m);
+  for (;;) {
+    WatchStager::Slot* s = nullptr;
+    for (;;) {
+      for (WatchStager::Slot& x : st.slots)
+        if (x.state == 1 && (!s || x.ticket < s->ticket)) s = &x;
+      if (s || st.stop) break;
+      st.cv_job.wait(g);
+    }
+    if (!s) return;
+    const gck_update* ups = s->ups;
+    size_t n = s->n;
+    g.unlock();
+    bool ok = false;
+    uint64_t gen = 0;
+    const std::vector<UpdateGroup>* groups = nullptr;
+    try {
+      bool part;
+      {
+        std::shared_lock<std::shared_mutex> sl(e.mu);
+        gen = e.shape_gen;
+        part = e.part_world > 1;
+        if (part) {  // (as apply_updates: the whole batch validated, then this rank's updates kept)
+          validate_updates(e, ups, n);
+          s->mine.clear();
+          for (size_t i = 0; i < n; ++i) {
+            const gck_tuple& t = ups[i].tuple;
+            if (part_keep(e, t.relation, t.resource_id, t.subject_id, t.subject_relation)) s->mine.push_back(ups[i]);
+          }
+        }
+      }
+      if (part) {
+        ups = s->mine.data();
+        n = s->mine.size();
+      }
+      groups = &group_updates(e, s->buf, ups, n, &e.mu);
+      ok = true;
+    } catch (...) {
+      ok = false;  // (gck_watch_apply_staged regroups it under the writer lock and reports the error)
+    }
+    g.lock();
+    s->ok = ok;
+    s->gen = gen;
+    s->groups = groups;
+    s->state = 2;
+    st.cv_done.notify_all();
+  }
+}
+
+int gck_watch_stage(gck_engine* ge, const gck_update* updates, size_t n, uint64_t* ticket) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    REQUIRE(ticket && (n == 0 || updates), GCK_E_INVALID_ARGUMENT, "null argument");
+    WatchStager& st = ge->stage;
+    std::lock_guard<std::mutex> g(st.m);
+    WatchStager::Slot* s = nullptr;
+    for (WatchStager::Slot& x : st.slots)
+      if (!x.ticket) {
+        s = &x;
+        break;
+      }
+    REQUIRE(s, GCK_E_CAPACITY, "every staging slot holds a batch: apply or discard one first");
+    if (!st.th.joinable()) st.th = std::thread(stager_loop, ge);
+    s->ups = updates;
+    s->n = n;
+    s->ticket = st.next_ticket++;
+    s->state = 1;
+    s->ok = false;
+    s->groups = nullptr;
+    *ticket = s->ticket;
+    st.cv_job.notify_all();
+  });
+}
+
+// Waits for the staged batch and frees its slot afterwards (whatever happens)
+struct StagedSlot {
+  WatchStager& st;
+  WatchStager::Slot* s = nullptr;
+  StagedSlot(WatchStager& w, uint64_t ticket) : st(w) {
+    std::unique_lock<std::mutex> g(st.m);
+    for (WatchStager::Slot& x : st.slots)
+      if (ticket && x.ticket == ticket) s = &x;
+    if (!s) throw Error(GCK_E_INVALID_ARGUMENT, "no staged Watch batch with ticket " + std::to_string(ticket));
+    st.cv_done.wait(g, [&] { return s->state == 2; });
+  }
+  ~StagedSlot() {
+    std::lock_guard<std::mutex> g(st.m);
+    s->ticket = 0;
+    s->state = 0;
+    s->groups = nullptr;
+  }
+};
+
+int gck_watch_apply_staged(gck_engine* ge, uint64_t revision, uint64_t ticket) {
+  return guard([&] {
+    Engine& e = need(ge);
+    need_schema(e);
+    StagedSlot ss(ge->stage, ticket);
+    PhaseClock pc("watch_call");
+    WriterLock wl(e);
+    pc.mark("lock");
+    // grouped against the engine's current shape: applied as staged; else (a write moved the
+    // shape since, or the staging failed) grouped again here, where any error is reported
+    if (ss.s->ok && ss.s->gen == e.shape_gen)
+      apply_updates(e, wl.lk, revision, ss.s->ups, ss.s->n, ss.s->groups);
+    else
+      apply_updates(e, wl.lk, revision, ss.s->ups, ss.s->n);
+    pc.mark("apply");
+  });
+}
+
+int gck_watch_discard(gck_engine* ge, uint64_t ticket) {
+  return guard([&] {
+    need(ge);
+    StagedSlot ss(ge->stage, ticket);
+  });
+}
+
 // What a text Watch batch may add before it is known to apply: new interned ids (CREATE of an
 // unseen object) and new caveat instances. A rejected batch takes them back, so that nothing of
 // it stays (interner counts are also the CSR row counts of the next batch).
@@ -610,6 +774,7 @@ static InternMark intern_mark(const Engine& e) {
 }
 
 static void intern_rollback(Engine& e, const InternMark& m) {
+  ++e.shape_gen;
   for (size_t t = 0; t < m.counts.size() && t < e.interner.size(); ++t) {
     TypeInterner& ti = e.interner[t];
     for (uint32_t id = m.counts[t]; id < ti.names.size(); ++id)
@@ -860,6 +1025,7 @@ int gck_set_partition(gck_engine* ge, uint32_t rank, uint32_t world) {
     e.part_rank = rank;
     e.part_world = world;
     e.part_set = true;
+    ++e.shape_gen;
     partition_rules(e);
     // the bundles and the bidirectional search need the whole graph; the membership indexes serve
     // the bundles: a partitioned rank's checks are decided by the partitioned label join from the

@@ -398,10 +398,17 @@ void validate_updates(const Engine& e, const gck_update* ups, size_t n) {
 // the key's top bits into ~one bucket per update, then an insertion sort of each bucket (a bucket
 // that a skewed batch fills is merge-sorted). Everything lives in Engine::group_buf and is reused
 // batch after batch (fresh vectors cost a 10K-update batch its allocations and page faults).
-const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, size_t n) {
+const std::vector<UpdateGroup>& group_updates(const Engine& e, GroupBuffers& B, const gck_update* ups, size_t n,
+                                              std::shared_mutex* schema_mu) {
   PhaseClock pc("group");
   if (n >= (1ull << 30)) throw Error(GCK_E_CAPACITY, "a Watch batch holds at most 2^30 updates");
-  GroupBuffers& B = e.group_buf;
+  // (a staged batch reads the schema and the interner under the engine lock, shared and briefly:
+  // once per new combination and for an update that fails its bounds)
+  auto locked = [&](auto&& f) {
+    if (!schema_mu) return f();
+    std::shared_lock<std::shared_mutex> sl(*schema_mu);
+    return f();
+  };
   struct KI {
     uint64_t k;  // (object << 32) | subject
     uint64_t i;  // update index << 34 | upsert << 33 | has expiration << 32 | caveat
@@ -423,7 +430,7 @@ const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, 
     return reinterpret_cast<KI*>(v.data());
   };
   std::vector<KI*> arr;
-  const uint32_t n_cav = (uint32_t)std::min<size_t>(e.caveat_instances.size(), 0xFFFFFFFFu);
+  const uint32_t n_cav = locked([&] { return (uint32_t)std::min<size_t>(e.caveat_instances.size(), 0xFFFFFFFFu); });
   for (size_t i = 0; i < n; ++i) {
     const gck_update& u = ups[i];
     if (u.op != GCK_UPDATE_CREATE && u.op != GCK_UPDATE_TOUCH && u.op != GCK_UPDATE_DELETE)
@@ -435,9 +442,14 @@ const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, 
     Slot& sl = cache[(combo * 0x9E3779B97F4A7C15ull) >> 58];
     if (sl.used && sl.combo == combo) {
       if (t.resource_id >= sl.rows || (!wild && t.subject_id >= sl.subs) || t.caveat >= n_cav)
-        validate_tuple(e, t);  // (raises the error)
+        locked([&] { validate_tuple(e, t); });  // (raises the error)
     } else {
-      validate_tuple(e, t);
+      uint32_t rows = 0, subs = 0;
+      locked([&] {
+        validate_tuple(e, t);
+        rows = e.interner[t.resource_type].count;
+        subs = e.interner[t.subject_type].count;
+      });
       const uint64_t gk = combo & 0xFFFFFFFFFFFFull;
       uint32_t k = 0;
       while (k < kinds.size() && kinds[k] != gk) ++k;
@@ -447,7 +459,7 @@ const std::vector<UpdateGroup>& group_updates(Engine& e, const gck_update* ups, 
         if (B.recs.size() <= k) B.recs.resize(k + 1);
         arr.push_back(recs(k));
       }
-      sl = Slot{combo, k, e.interner[t.resource_type].count, e.interner[t.subject_type].count, 1u};
+      sl = Slot{combo, k, rows, subs, 1u};
     }
     const uint32_t k = sl.kind;
     const uint64_t up = u.op != GCK_UPDATE_DELETE ? 1 : 0;

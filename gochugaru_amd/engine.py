@@ -176,6 +176,9 @@ _SIGS = {
     "gck_device_bytes": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "gck_apply_updates": (C.c_int, [_P, C.c_uint64, _P, C.c_size_t]),
     "gck_apply_updates_text": (C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
+    "gck_watch_stage": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_uint64)]),
+    "gck_watch_apply_staged": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
+    "gck_watch_discard": (C.c_int, [_P, C.c_uint64]),
     "gck_check_bulk": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.c_int64, _P, _P]),
     "gck_check_bulk_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int64, _P, _P, _P]),
     "gck_check_bulk_ctx": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.POINTER(C.c_char_p),
@@ -348,6 +351,7 @@ class Engine:
         self._lib = lib
         self._pins = 0          # live host_array() buffers (each keeps the engine handle alive)
         self._closing = False
+        self._staged = {}       # ticket -> the staged Watch batch's array (kept alive until applied)
         self._type_ids = {}
         self._rel_ids = {}
         self.part_rank, self.part_world = 0, 1
@@ -529,6 +533,30 @@ class Engine:
         updates = np.ascontiguousarray(updates, dtype=UPDATE_DTYPE)
         _check(self._lib.gck_apply_updates(self._h, revision, updates.ctypes.data if len(updates) else None,
                                            len(updates)))
+
+    def stage_updates(self, updates: np.ndarray) -> int:
+        """Stages a batch (gck_watch_stage): the engine's thread validates and groups it while the
+        caller applies the previous one. Returns the ticket for `apply_staged`; the array is held
+        until then."""
+        updates = np.ascontiguousarray(updates, dtype=UPDATE_DTYPE)
+        t = C.c_uint64(0)
+        _check(self._lib.gck_watch_stage(self._h, updates.ctypes.data if len(updates) else None, len(updates),
+                                         C.byref(t)))
+        self._staged[t.value] = updates
+        return t.value
+
+    def apply_staged(self, revision: int, ticket: int):
+        """Applies a staged batch -> `revision` (gck_watch_apply_staged; the errors of apply_updates)."""
+        try:
+            _check(self._lib.gck_watch_apply_staged(self._h, revision, ticket))
+        finally:
+            self._staged.pop(ticket, None)
+
+    def discard_staged(self, ticket: int):
+        try:
+            _check(self._lib.gck_watch_discard(self._h, ticket))
+        finally:
+            self._staged.pop(ticket, None)
 
     def apply_updates_text(self, revision: int, text: str):
         """One batch as text: "<CREATE|TOUCH|DELETE> <rel.Relationship.String>" per line."""

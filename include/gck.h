@@ -19,7 +19,7 @@
  *   gck_intern
  *       replaces the per-item string handling of Client.Check's item loop
  *       (client/client.go:242-259) with batched string -> dense u32 interning.
- *   gck_apply_updates / gck_apply_updates_text
+ *   gck_apply_updates / gck_apply_updates_text (or gck_watch_stage + gck_watch_apply_staged)
  *       consume the rel.Update stream of Client.UpdatesSinceRevision (client/client.go:370-413,
  *       rel.UpdateFromV1Proto rel/relationship.go:296-301) and keep the snapshot current.
  *   gck_check_bulk_ctx / gck_check_bulk_device_ctx
@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 11
+#define GCK_ABI_VERSION 12
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -302,6 +302,16 @@ int gck_apply_updates(gck_engine* e, uint64_t revision, const gck_update* update
 /* Text form: one "<OP> <relationship>" per line, OP = CREATE | TOUCH | DELETE and the
  * relationship in rel.Relationship.String form (rel/relationship.go:51-90). */
 int gck_apply_updates_text(gck_engine* e, uint64_t revision, const char* text, size_t len);
+/* Pipelined Watch: a consumer that has the next batch while it applies the previous one stages it
+ * — gck_watch_stage returns at once and an engine thread validates and groups the batch meanwhile
+ * — then applies it with gck_watch_apply_staged, in stream order, which waits for the grouping and
+ * applies as gck_apply_updates does (same errors; a batch the staging rejected, or staged before a
+ * schema / snapshot-file / partition change, is grouped again there and its error reported).
+ * `updates` must stay valid and unchanged until the ticket is applied or discarded. Up to 4
+ * batches may be staged at once (GCK_E_CAPACITY beyond); a ticket is used once. */
+int gck_watch_stage(gck_engine* e, const gck_update* updates, size_t n, uint64_t* ticket);
+int gck_watch_apply_staged(gck_engine* e, uint64_t revision, uint64_t ticket);
+int gck_watch_discard(gck_engine* e, uint64_t ticket);
 
 /* ---- checks (CheckBulkPermissions, client/client.go:261-283) -------------------------- */
 /* Host buffers: items[n] in, out_perm[n] (GCK_PERM_*), out_err[n] (GCK_ITEM_*) out.

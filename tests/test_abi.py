@@ -45,7 +45,7 @@ def test_struct_layouts_match_header():
     assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
     assert C.sizeof(E._Stats) == 232
-    assert E.load_library().gck_abi_version() == 11
+    assert E.load_library().gck_abi_version() == 12
 
 
 @pytest.fixture()
@@ -150,3 +150,27 @@ def test_state_errors(eng):
     with pytest.raises(E.GckError) as ei:
         eng.apply_updates(2, np.zeros(1, dtype=E.UPDATE_DTYPE))
     assert ei.value.code == E.GCK_E_STATE
+
+
+def test_watch_staging_without_a_snapshot():
+    """gck_watch_stage works on the host alone (validation and grouping on the engine's thread);
+    applying needs a committed snapshot (GCK_E_STATE); four slots; unknown tickets refused."""
+    from gochugaru_amd import engine as E
+    e = E.Engine()
+    e.load_schema("definition user {}\ndefinition group { relation member: user }")
+    ups = np.zeros(2, dtype=E.UPDATE_DTYPE)
+    ups["op"] = E.UPDATE_CREATE
+    ts = [e.stage_updates(ups) for _ in range(4)]
+    with pytest.raises(E.GckError) as ei:
+        e.stage_updates(ups)
+    assert ei.value.code == E.GCK_E_CAPACITY
+    with pytest.raises(E.GckError) as ei:
+        e.apply_staged(2, ts[0])
+    assert ei.value.code == E.GCK_E_STATE
+    for t in ts[1:]:
+        e.discard_staged(t)
+    with pytest.raises(E.GckError) as ei:
+        e.discard_staged(ts[1])
+    assert ei.value.code == E.GCK_E_INVALID_ARGUMENT
+    e.stage_updates(ups)  # (a slot is free again; the engine ends with a batch still staged)
+    e.close()

@@ -248,3 +248,91 @@ def test_skewed_batch_on_one_object():
     assert engine_results(e, checks) == oracle_results(schema, store, checks)
     assert e.tuple_count == len(store)
     e.close()
+
+
+def _records(e, ops):
+    """(op, tuple line) -> gck_update records (new object names interned first)."""
+    ups = np.zeros(len(ops), dtype=E.UPDATE_DTYPE)
+    for i, (op, line) in enumerate(ops):
+        t = ref.parse_tuple(line)
+        rt, st = e.type_id(t.resource_type), e.type_id(t.subject_type)
+        ups[i]["op"] = {"CREATE": E.UPDATE_CREATE, "TOUCH": E.UPDATE_TOUCH, "DELETE": E.UPDATE_DELETE}[op]
+        tt = ups[i]["tuple"]
+        tt["resource_type"], tt["relation"] = rt, e.relation_id(rt, t.relation)
+        tt["resource_id"] = e.intern(rt, [t.resource_id], create=True)[0]
+        tt["subject_type"] = st
+        srel = t.subject_relation
+        tt["subject_relation"] = e.relation_id(st, srel) if srel and srel != "..." else E.ELLIPSIS
+        tt["subject_id"] = e.intern(st, [t.subject_id], create=True)[0]
+        ups[i]["tuple"] = tt
+    return ups
+
+
+@pytest.mark.parametrize("family", ["nested", "gdocs"])
+def test_staged_watch_batches(family):
+    """Pipelined Watch (gck_watch_stage / gck_watch_apply_staged): each batch is staged while the
+    previous one applies, two ahead at times; results after every batch equal the oracle's on the
+    same store. A staged batch the staging rejects fails at its apply (nothing applied, the
+    revision stays); a discarded ticket is gone."""
+    schema, tuples, _ = gen.FAMILIES[family](4)
+    rng = random.Random(23)
+    e = E.Engine()
+    e.load_schema(schema)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    store = {}
+    apply_to_store(store, [("CREATE", t) for t in tuples])
+    # batches over names the snapshot already holds (interned before staging)
+    plan = []
+    for rnd in range(6):
+        ups = [(op, l) for op, l in random_batch(rng, family, dict(store), rnd) if "_n" not in l.split("#")[0]]
+        plan.append(ups)
+    recs = [None] * len(plan)
+    recs[0] = _records(e, plan[0])
+    tickets = [e.stage_updates(recs[0])]
+    rev = 1
+    for k, ups in enumerate(plan):
+        if k + 1 < len(plan):
+            recs[k + 1] = _records(e, plan[k + 1])
+            tickets.append(e.stage_updates(recs[k + 1]))
+        rev += 1
+        e.apply_staged(rev, tickets[k])
+        apply_to_store(store, ups)
+        assert e.revision == rev and e.tuple_count == len(store), k
+        checks = checks_for(family, 4, store, ups)
+        assert engine_results(e, checks) == oracle_results(schema, store, checks), k
+    # a rejected staged batch: an unknown operation
+    bad = _records(e, plan[0][:3])
+    bad[1]["op"] = 77
+    t = e.stage_updates(bad)
+    with pytest.raises(E.GckError) as ei:
+        e.apply_staged(rev + 1, t)
+    assert ei.value.code == E.GCK_E_INVALID_ARGUMENT and e.revision == rev
+    # staged, then discarded: never applied
+    t = e.stage_updates(_records(e, plan[1]))
+    e.discard_staged(t)
+    with pytest.raises(E.GckError):
+        e.apply_staged(rev + 1, t)
+    assert e.revision == rev
+    e.close()
+
+
+def test_staging_slots_and_tickets():
+    """Up to four batches staged at once; a ticket is applied once; the staging thread ends with
+    the engine."""
+    schema, tuples, _ = gen.nested(2)
+    e = E.Engine()
+    e.load_schema(schema)
+    e.load_snapshot_text(1, "\n".join(tuples))
+    line = [l for l in tuples if "@user:" in l][0]
+    recs = _records(e, [("TOUCH", line)])
+    ts = [e.stage_updates(recs) for _ in range(4)]
+    with pytest.raises(E.GckError) as ei:
+        e.stage_updates(recs)
+    assert ei.value.code == E.GCK_E_CAPACITY
+    for i, t in enumerate(ts):
+        e.apply_staged(2 + i, t)
+    with pytest.raises(E.GckError) as ei:
+        e.apply_staged(9, ts[0])
+    assert ei.value.code == E.GCK_E_INVALID_ARGUMENT
+    assert e.revision == 5
+    e.close()
