@@ -992,8 +992,14 @@ def main():
         # the rest of the step (watch.apply_ms_per_step)
         ms_a = (st["bundle_ms"] + st["giant_ms"]) / st["bundle_launches"]
         achieved = mixed_alg / (ms_a * 1e-3) / 1e9
+        # (the counter passes of config 5's own check batches, tools/gpu.sh profile ... --config mixed)
+        tj_path = args.traffic_json or os.path.join(ROOT, "profiles", "r05", "pmc_mixed", "traffic.json")
+        m_traffic, m_src = None, None
+        if os.path.exists(tj_path):
+            m_traffic = json.load(open(tj_path)).get("hbm_bytes_per_batch")
+            m_src = os.path.relpath(tj_path, os.path.dirname(os.path.abspath(__file__)))
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": m_traffic, "traffic_source": m_src,
                 "kernel": ("stage A of the check batch: k_label_join with the caveat plane, then k_bundles<1> over "
                            "the checks it deferred" if st["label_checks"] > 0 else
                            "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks)")

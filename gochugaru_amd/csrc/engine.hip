@@ -242,6 +242,8 @@ struct Workspace {
   DevCounters* h_ctr = nullptr;  // pinned, coherent (k_publish writes it)
   unsigned* h_seq = nullptr;     // after h_ctr + bundle counters: the last published batch
   unsigned pub_seq = 0;
+  uint64_t patch_seen = 0;       // the engine's index-patch sequence this workspace's stream waited for
+  void* patch_stream = nullptr;  // ... on this stream (make_ctx)
   unsigned* d_hpub = nullptr;    // device address of h_ctr
   bool ctr_clean = false;        // ctr + b_ctrs are zero (k_publish left them so)
   gck_item* d_items = nullptr;   // staging for the host-buffer API
@@ -1420,6 +1422,9 @@ int device_init(Engine& e) {
   hipEvent_t sev = nullptr;
   HIP_OK(hipEventCreateWithFlags(&sev, hipEventDisableTiming));
   e.sync_ev = sev;
+  hipEvent_t pev = nullptr;
+  HIP_OK(hipEventCreateWithFlags(&pev, hipEventDisableTiming));
+  e.patch_ev = pev;
   e.device_ready = true;
   return 0;
 }
@@ -1520,6 +1525,9 @@ void device_free(Engine& e) {
     e.delta_ev = nullptr;
     if (e.sync_ev) (void)hipEventDestroy((hipEvent_t)e.sync_ev);
     e.sync_ev = nullptr;
+    if (e.patch_ev) (void)hipEventDestroy((hipEvent_t)e.patch_ev);
+    e.patch_ev = nullptr;
+    e.patch_seq = 0;
     if (e.blob_host) (void)hipHostFree(e.blob_host);
     e.blob_host = nullptr;
     e.blob_host_cap = 0;
@@ -1706,8 +1714,12 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
     // only — a device-wide synchronisation would also wait for the check batches running on the
     // engine's non-blocking streams beside the build (config 5: ~55 us of a 0.29 ms Watch batch)
     pc.mark("csr_loop");
-    if (delta) spin_stream(e, nullptr);
-    else HIP_OK(hipDeviceSynchronize());
+    // (a Watch batch does not wait here: what follows reads the merged arrays on the null stream
+    // after the merge, or through a synchronous copy that waits for it; the publication waits for
+    // the null stream before the snapshot is swapped in, device_apply_publish)
+    static const bool dbg_csr_sync = getenv("GCK_DEBUG_CSR_SYNC") != nullptr;
+    if (!delta) HIP_OK(hipDeviceSynchronize());
+    else if (dbg_csr_sync) spin_stream(e, nullptr);
     pc.mark("csr_sync");
     // link the node program to the CSR table
     std::vector<DevItem> items = sc.items;
@@ -2057,7 +2069,16 @@ void release_ws(Engine& e, Workspace* w) {
   e.ws_cv.notify_all();  // a two-workspace caller may be waiting beside one-workspace callers
 }
 
-static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us) {
+// A Watch batch's membership-index patch runs on the null stream after its publication, not
+// waited for (delta.inc device_apply_publish): every launch that may probe the indexes — the wave
+// bundles, the level loop, the lookups; the joins do not — is ordered after it on the GPU by its
+// stream waiting for the patch's event (once per workspace, stream and patch).
+static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us, hipStream_t st) {
+  if (e.patch_seq && (w.patch_seen != e.patch_seq || w.patch_stream != (void*)st)) {
+    HIP_OK(hipStreamWaitEvent(st, (hipEvent_t)e.patch_ev, 0));
+    w.patch_seen = e.patch_seq;
+    w.patch_stream = (void*)st;
+  }
   DeviceSnapshot& ds = *e.dev;
   Ctx c{};
   c.nodes = ds.nodes;
@@ -2140,7 +2161,7 @@ static bool run_batch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t
                       uint8_t* d_perm, int32_t* d_err, hipStream_t st, float* ms_out, size_t pos,
                       const uint32_t* map) {
   ensure_wide(w);
-  Ctx c = make_ctx(e, w, now_us);
+  Ctx c = make_ctx(e, w, now_us, st);
   c.ck_items = d_items;
   c.ck_map = map;
   c.ck_off = map ? 0u : (uint32_t)pos;
@@ -2357,7 +2378,7 @@ static bool label_join_on(const Engine& e) {
 
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
-  Ctx c = make_ctx(e, w, now_us);
+  Ctx c = make_ctx(e, w, now_us, st);
   c.ck_items = d_items;
   BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
@@ -2404,7 +2425,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
                       w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
                       ((aql_timed && e.aql->tick_hz) || !w.b_timed);
   w.b_aql = false;
-  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok);
+  // (GCK_DEBUG_HIP_SELFPUB: an engine-stream batch launched through HIP publishes itself from its
+  // last block as an AQL-dispatched one does — the dispatch-span attribution of tools/aql_span.sh;
+  // its results are not written back before the publication, so only device readers may use them)
+  static const bool dbg_selfpub = getenv("GCK_DEBUG_HIP_SELFPUB") != nullptr;
+  const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok || dbg_selfpub);
   const uint32_t coherent = 0u;  // (results are published by the kernel end's write-back)
   // the join into the HSA queue when aql_ok and the code object has this variant
   auto aql_try = [&](const char* name, const void* args, size_t bytes, uint32_t blocks) {
@@ -2600,7 +2625,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   if (n_cj > 0 && !w.b_chained) {
     // the checks the closure join left: the wave bundles over its list (the publish zeroed the
     // count on the device: restore it first)
-    Ctx c = make_ctx(e, w, now_us);
+    Ctx c = make_ctx(e, w, now_us, st);
     c.ck_items = d_items;
     BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
     a.idx = w.c_deferred;
@@ -2634,7 +2659,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     // stage B: giant checks, one 16-wave workgroup each, over stage A's deferred list (the
     // publish zeroed the deferred count on the device: restore it first)
     ensure_giant(w);
-    Ctx c = make_ctx(e, w, now_us);
+    Ctx c = make_ctx(e, w, now_us, st);
     c.ck_items = d_items;
     BundleArgs g = bundle_args(e, w, d_items, n, d_perm, d_err);
     g.idx = w.b_deferred;

@@ -1,6 +1,12 @@
 // gck_api.cpp — the extern "C" boundary (include/gck.h). Every entry point converts C++
 // exceptions into a negative status plus a thread-local message (gck_last_error).
+#include <pthread.h>
+#include <sched.h>
+
+#include <algorithm>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -634,8 +640,54 @@ int gck_apply_updates(gck_engine* ge, uint64_t revision, const gck_update* updat
   });
 }
 
+// The CPUs of a sysfs cpu list ("0-7,64-71").
+static std::vector<int> cpu_list(const char* path) {
+  std::vector<int> out;
+  FILE* f = std::fopen(path, "r");
+  if (!f) return out;
+  char buf[4096];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  for (char* p = buf; *p;) {
+    char* end;
+    const long a = std::strtol(p, &end, 10);
+    if (end == p) break;
+    long b = a;
+    if (*end == '-') b = std::strtol(end + 1, &end, 10);
+    for (long c = a; c <= b && c < 65536; ++c) out.push_back((int)c);
+    p = *end ? end + 1 : end;
+  }
+  return out;
+}
+
+// Places the stager on the applying thread's last-level cache (its L3 domain minus its own core):
+// the applying thread reads every record the stager wrote, which then stays in that cache instead
+// of crossing between core complexes (config 5: ~30 us of a 0.2 ms step). Left to the scheduler
+// when the topology cannot be read.
+static void stager_place(int caller_cpu) {
+  if (caller_cpu < 0) return;
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", caller_cpu);
+  std::vector<int> l3 = cpu_list(path);
+  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", caller_cpu);
+  const std::vector<int> sib = cpu_list(path);
+  cpu_set_t allowed;
+  if (l3.empty() || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int n = 0;
+  for (int c : l3)
+    if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed) && std::find(sib.begin(), sib.end(), c) == sib.end()) {
+      CPU_SET(c, &set);
+      ++n;
+    }
+  if (n) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
 // The stager's thread: groups the queued batches in ticket order.
-static void stager_loop(gck_engine* ge) {
+static void stager_loop(gck_engine* ge, int caller_cpu) {
+  if (!getenv("GCK_STAGER_ANYWHERE")) stager_place(caller_cpu);
   Engine& e = ge->impl;
   WatchStager& st = ge->stage;
   std::unique_lock<std::mutex> g(st.m);
@@ -701,7 +753,7 @@ int gck_watch_stage(gck_engine* ge, const gck_update* updates, size_t n, uint64_
         break;
       }
     REQUIRE(s, GCK_E_CAPACITY, "every staging slot holds a batch: apply or discard one first");
-    if (!st.th.joinable()) st.th = std::thread(stager_loop, ge);
+    if (!st.th.joinable()) st.th = std::thread(stager_loop, ge, sched_getcpu());
     s->ups = updates;
     s->n = n;
     s->ticket = st.next_ticket++;

@@ -31,4 +31,5 @@ run aql_hostargs GCK_DEBUG_AQL_HOSTARGS=1
 run aql_noprof GCK_DEBUG_AQL_NOPROF=1
 run aql_single GCK_DEBUG_AQL_SINGLE=1
 run aql_signal GCK_DEBUG_AQL_SIGNAL=1
+run hip_selfpub GCK_AQL=0 GCK_DEBUG_HIP_SELFPUB=1
 GCK_DEBUG_AQL=1 timeout -k 10 200 python3 tools/host_probe.py --phases device --lone 5 --batches 10 2>&1 | grep "gck aql\] k_closure" | head -3
