@@ -245,7 +245,18 @@ def test_skewed_batch_on_one_object():
             for _ in range(600)]
     e.apply_updates_text(9, "\n".join(f"{op} {line}" for op, line in ups))
     apply_to_store(store, ups)
-    assert engine_results(e, checks) == oracle_results(schema, store, checks)
+    got, want = engine_results(e, checks), oracle_results(schema, store, checks)
+    bad = [i for i in range(len(checks)) if got[i] != want[i]]
+    if bad:  # (what a fresh engine over the same relationships answers, for the report)
+        f = E.Engine()
+        f.load_schema(schema)
+        f.load_snapshot_text(9, "\n".join(store.values()))
+        fresh = engine_results(f, [checks[i] for i in bad])
+        f.close()
+        again = engine_results(e, checks)
+        pytest.fail("after the large batch: " + "; ".join(
+            f"{checks[i]} got {got[i]} want {want[i]} fresh {fresh[k]} again {again[i]}" for k, i in enumerate(bad[:8]))
+            + f" ({len(bad)} of {len(checks)}; stats {e.stats()})")
     assert e.tuple_count == len(store)
     e.close()
 
