@@ -99,6 +99,9 @@ def parse():
                          "tuples, check contexts, one Watch batch of --churn x tuples applied per step); quota = "
                          "config 5 with 32K per-relationship caveat contexts x one context per request")
     ap.add_argument("--selftest", action="store_true", help="launcher / rank bookkeeping only (no GPU; tests)")
+    ap.add_argument("--coalesce", type=int, default=None,
+                    help="strong scaling: a rank checks its slices of up to this many consecutive requests in one "
+                         "dispatch (default: the ranks, so a dispatch is again ~--batch checks; 1 = one per request)")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--watch-stage", type=int, default=1,
                     help="config 5: stage the next step's Watch batch (gck_watch_stage: grouped on the engine's "
@@ -510,9 +513,20 @@ def main():
         s_lo, s_hi = slices(args.batch, world)[rank]
         n_slice = s_hi - s_lo
         n_rot = args.warm + args.steps
-        rot = [WL.checks(args.batch, 1000 + k)[s_lo:s_hi].contiguous() for k in range(n_rot)]
-        outs = [(torch.zeros(n_slice, dtype=torch.uint8, device=dev),
-                 torch.zeros(n_slice, dtype=torch.int32, device=dev)) for _ in range(n_rot)]
+        # (one device array for every rotated slice and one per result plane: a rank's slices of
+        # consecutive requests lie back to back, so several can go in one dispatch)
+        rot_all = torch.cat([WL.checks(args.batch, 1000 + k)[s_lo:s_hi] for k in range(n_rot)]).contiguous()
+        rot = [rot_all[k * n_slice:(k + 1) * n_slice] for k in range(n_rot)]
+        perm_all = torch.zeros(n_rot * n_slice, dtype=torch.uint8, device=dev)
+        err_all = torch.zeros(n_rot * n_slice, dtype=torch.int32, device=dev)
+        outs = [(perm_all[k * n_slice:(k + 1) * n_slice], err_all[k * n_slice:(k + 1) * n_slice]) for k in range(n_rot)]
+        # Coalescing (strong scaling): with N ranks a request leaves each rank ~batch/N checks, and
+        # a dispatch that small is bound by its own latency, not by the GPU; a rank therefore checks
+        # its slices of up to `coal` consecutive requests in one dispatch (they are contiguous), as a
+        # node-level dispatcher batches what arrives for each GPU. The timed region still holds
+        # exactly the steps' requests. coal_for(count): the largest divisor of count <= coal.
+        coal = max(1, min(args.coalesce if args.coalesce else world, max(1, args.batch // max(1, n_slice))))
+        coal_for = lambda count: max(c for c in range(1, coal + 1) if count % c == 0)
         streams = [torch.cuda.Stream(dev) for _ in range(depth)]
         # `value`'s path (BASELINE.md:40-41, SURVEY §8d: items H2D + kernels + results D2H): the
         # same requests in host memory — pinned, from gck_host_alloc, where a cgo caller builds its
@@ -549,10 +563,11 @@ def main():
 
             def prepare(count):
                 k0 = cursor["k"] + sum(c for c, _ in prepared.values())
-                ks = range(k0, k0 + count)
+                cc = coal_for(count)
+                ks = range(k0, k0 + count, cc)
                 prepared[len(prepared)] = (count, eng.prepare_batches(
                     [h_ptr(h_items, k) for k in ks], [h_ptr(h_perm, k) for k in ks], [h_ptr(h_err, k) for k in ks],
-                    n_slice, depth, host=True))
+                    n_slice * cc, depth, host=True))
 
             def run_steps(count):
                 c, run = prepared.pop(min(prepared))
@@ -608,11 +623,14 @@ def main():
     # of their own, on the engine's streams.
     device_resident = None
     if pipelined:
-        mkd = lambda ks: eng.prepare_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
-                                             [outs[k][1].data_ptr() for k in ks], n_slice, depth,
-                                             [streams[j % depth].cuda_stream for j in range(len(ks))],
-                                             engine_streams=bool(args.engine_streams))
-        d_warm, d_run = mkd(range(args.warm)), mkd(range(args.warm, args.warm + args.steps))
+        def mkd(k0, count):
+            cc = coal_for(count)
+            ks = range(k0, k0 + count, cc)
+            return eng.prepare_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
+                                       [outs[k][1].data_ptr() for k in ks], n_slice * cc, depth,
+                                       [streams[j % depth].cuda_stream for j in range(len(ks))],
+                                       engine_streams=bool(args.engine_streams))
+        d_warm, d_run = mkd(0, args.warm), mkd(args.warm, args.steps)
         torch.cuda.synchronize()
         d_warm.run()
         torch.cuda.synchronize()
@@ -1108,6 +1126,9 @@ def main():
                                                                   if spicedb else
                                                                   "none was found, so the C restatement stands in")}}
                              if cpu else cpu),
+            **({"dispatch": {"requests_per_dispatch": coal_for(args.steps), "checks_per_dispatch": n_slice * coal_for(args.steps),
+                             "note": "a rank's slices of consecutive requests checked in one dispatch (--coalesce)"}}
+               if strong and world > 1 else {}),
             **({"baseline_pipelined": baseline_pipelined} if baseline_pipelined else {}),
             **({"baseline_step": baseline_step} if baseline_step else {}),
             **({"weak_scaling": weak} if weak else {}),

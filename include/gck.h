@@ -396,15 +396,18 @@ int gck_lookup_subjects(gck_engine* e, const gck_consistency* cs, uint16_t resou
                         uint32_t* out_ids, uint8_t* out_perm, size_t cap, size_t* out_n);
 
 /* ---- partitioned graphs (graphs above one GPU's 288 GB) ----------------
- * Rank r of `world` (one process per GPU) owns the objects with gck_partition_owner(id) == r
- * (id mod world) and holds only (every ingest path filters — gck_add_tuples*, gck_load_csr,
- * gck_apply_updates* — after interning, so ids and caveat instances agree on every rank; every
- * rank reads the whole export / Watch stream, none stores another rank's rows):
+ * Rank r of `world` (one process per GPU) owns the objects whose names hash to it
+ * (gck_partition_owner_name, below: decided from the name, before anything is interned; the
+ * owner gives the id, local * world + r, so gck_partition_owner(id) = id mod world names the same
+ * rank). Every rank reads the whole export / Watch stream and keeps only (every ingest path
+ * filters — gck_part_add_tuples_text_with, gck_add_tuples, gck_load_csr, gck_apply_updates —
+ * none stores another rank's rows):
  *   - the relationships of the objects it owns;
  *   - the schema's hub hierarchy (the userset and wildcard relationships of "hub" relations —
  *     nested groups, teams — which usersets and arrows point at and which allow no caveat or
  *     expiration), replicated;
- *   - the hub relationships of the subjects it owns (their side of the label join).
+ *   - the direct hub memberships of the subjects it owns (their side of the label join: a hub
+ *     membership goes to its subject's owner, not its object's).
  * All ranks then check one batch together — every rank calls with the same items and gets every
  * result: the label join (a subject's owner sends its slot to the resource's owner, which decides
  * the check), then an exact-depth level loop over what it left, with intersection, exclusion,
