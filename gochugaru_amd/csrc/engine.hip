@@ -219,6 +219,7 @@ struct Workspace {
   bool b_timed = false;       // this batch's stage A is bracketed by ev0 / ev1 (GCK_FLAG_PROFILE, sampled)
   bool b_own_stream = false;  // a device batch on the workspace's stream (GCK_SUBMIT_ENGINE_STREAM)
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
+  uint32_t b_sum_blocks = 0;  // ... in that many blocks, each with a summary slot (closure.inc block_summary)
   bool b_validate = false;    // host items read in place: the join checks their context slots
   void* aql_kernarg = nullptr;  // aql.inc: kernarg block of the dispatched join (pinned host memory, or VRAM)
   bool aql_devargs = false;     // ... in VRAM (aql.inc AqlState::devargs)
@@ -245,6 +246,9 @@ struct Workspace {
   uint64_t patch_seen = 0;       // the engine's index-patch sequence this workspace's stream waited for
   void* patch_stream = nullptr;  // ... on this stream (make_ctx)
   unsigned* d_hpub = nullptr;    // device address of h_ctr
+  unsigned* h_slots = nullptr;   // pinned: {deferred, counters touched} per block of an AQL-dispatched join
+  unsigned* d_slots = nullptr;   // (device address)
+  uint32_t n_slots = 0;
   bool ctr_clean = false;        // ctr + b_ctrs are zero (k_publish left them so)
   gck_item* d_items = nullptr;   // staging for the host-buffer API
   uint8_t* d_perm = nullptr;
@@ -1464,6 +1468,7 @@ static void free_workspace(Workspace* w) {
   free_part(w->part);
   free_list(w->allocs);
   if (w->h_ctr) (void)hipHostFree(w->h_ctr);
+  if (w->h_slots) (void)hipHostFree(w->h_slots);
   if (w->h_items) (void)hipHostFree(w->h_items);
   if (w->h_ctx) (void)hipHostFree(w->h_ctx);
   if (w->dbg) (void)hipFree(w->dbg);
@@ -1931,6 +1936,11 @@ static Workspace* create_workspace(Engine& e) {
     w->h_seq = w->h_bctrs + kBCtrs;
     *w->h_seq = 0;
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&w->d_hpub), w->h_ctr, 0));
+    // the block summaries of AQL-dispatched joins: one 8-B slot per block (>= 64 checks per block)
+    w->n_slots = (uint32_t)(w->max_batch / 64 + 2);
+    HIP_OK(hipHostMalloc(&w->h_slots, (size_t)w->n_slots * 8, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(w->h_slots, 0, (size_t)w->n_slots * 8);
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&w->d_slots), w->h_slots, 0));
     // pinned staging of host batches: 20 B of items in, 5 B of results out per check
     const size_t stage = w->max_batch * (sizeof(gck_item) + 1 + 4);
     void* hs = nullptr;
@@ -2376,6 +2386,41 @@ static bool label_join_on(const Engine& e) {
   return ds.d_lj && (!(ds.d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE)) || ds.lj_preferred);
 }
 
+// An AQL-dispatched join reports through per-block summaries (closure.inc block_summary): its
+// arguments point at the workspace's slots, and its deferred-list counter is one of two words that
+// alternate per batch (b_ctrs[6 + (seq & 1)]; the join clears the other for the next batch).
+static void aql_summaries(Workspace& w, uint32_t& coherent, unsigned*& h_out, unsigned*& clear, unsigned*& n_deferred,
+                          uint32_t blocks) {
+  if (blocks > w.n_slots) return;  // (kept on the last-block publication)
+  const uint32_t e = w.pub_seq & 1u;
+  coherent |= kPubBySignal;
+  h_out = w.d_slots;
+  n_deferred = w.b_ctrs + 6 + e;
+  clear = w.b_ctrs + 6 + (e ^ 1u);
+  w.b_sum_blocks = blocks;
+}
+
+// After the completion signal: the batch's counters from its blocks' summaries into the host copy
+// the rest of the engine reads (*h_ctr, h_bctrs[4]); the device counters only when a block touched
+// them (task rounds, probes, a bad context slot), read and cleared synchronously.
+static void aql_collect(Workspace& w) {
+  uint64_t* slot = reinterpret_cast<uint64_t*>(w.h_slots);
+  uint32_t deferred = 0, touched = 0;
+  for (uint32_t b = 0; b < w.b_sum_blocks; ++b) {
+    const uint64_t v = slot[b];
+    if (!v) continue;
+    deferred += (uint32_t)v;
+    touched |= (uint32_t)(v >> 32);
+    slot[b] = 0;
+  }
+  std::memset(w.h_ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned));
+  if (touched) {
+    HIP_OK(hipMemcpy(w.h_ctr, w.ctr, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(w.ctr, 0, sizeof(DevCounters)));
+  }
+  w.h_bctrs[4] = deferred;
+}
+
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   Ctx c = make_ctx(e, w, now_us, st);
@@ -2425,6 +2470,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
                       w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
                       ((aql_timed && e.aql->tick_hz) || !w.b_timed);
   w.b_aql = false;
+  w.b_sum_blocks = 0;
   // (GCK_DEBUG_HIP_SELFPUB: an engine-stream batch launched through HIP publishes itself from its
   // last block as an AQL-dispatched one does — the dispatch-span attribution of tools/aql_span.sh;
   // its results are not written back before the publication, so only device readers may use them)
@@ -2497,8 +2543,9 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.cx = w.d_ctx;
     }
     if (ak) {
-      if (j.h_out) j.coherent |= kPubBySignal;
-      aql_dispatch(*e.aql, w, *ak, &j, sizeof(j), (n + 32u * kWaves - 1) / (32u * kWaves), w.b_timed,
+      const uint32_t blocks = (n + 32u * kWaves - 1) / (32u * kWaves);
+      if (j.h_out) aql_summaries(w, j.coherent, j.h_out, j.done, j.n_deferred, blocks);
+      aql_dispatch(*e.aql, w, *ak, &j, sizeof(j), blocks, w.b_timed,
                    cav ? &c : nullptr, cav ? sizeof(Ctx) : 0);
       w.b_aql = true;
     } else {
@@ -2553,7 +2600,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     static_assert(offsetof(decltype(cj_args), j) == 344, "k_closure_join kernarg layout (Ctx, CjArgs)");
     // (half slots: the first 32 B of each resource slot, closure.inc HALF)
     if (fast && aql_ok && j.h_out && aql_kernel(e.aql, "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)"))
-      cj_args.j.coherent |= kPubBySignal;
+      aql_summaries(w, cj_args.j.coherent, cj_args.j.h_out, cj_args.j.done, cj_args.j.n_deferred, grid.x);
     if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
                         sizeof(cj_args), grid.x)) {
     } else if (fast)
@@ -2592,7 +2639,8 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n);
 static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   if (w.b_aql) aql_wait(*e.aql, w);  // (the kernel has ended: its publication is complete)
-  wait_published(w, st, w.b_seq);
+  if (w.b_aql && w.b_sum_blocks) aql_collect(w);
+  else wait_published(w, st, w.b_seq);
   add_counters(e, w, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
   if (w.h_ctr->bad_slot) {  // (a zero-copy batch's join found a context slot out of range)
