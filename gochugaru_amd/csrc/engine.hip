@@ -2332,7 +2332,8 @@ static BundleArgs bundle_args(Engine& e, Workspace& w, const gck_item* d_items, 
   // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
   // bundle records of stages A and B, then the closure join's per-wave records
-  const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2 + (size_t)kCjTimingWords * (n / 64 + 1);
+  const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2 +
+                              std::max((size_t)kCjTimingWords * (n / 64 + 1), (size_t)kLjTimingWords * (n / 16 + 1));
   if (timing_env && w.timing_cap < timing_words) {
     if (w.timing) (void)hipFree(w.timing);
     w.timing = nullptr;
@@ -2512,6 +2513,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.cav_n = ds.n_cav;
       j.cav_rows = rows;
     }
+    j.timing = a.timing ? a.timing + (size_t)kTimingWords * (n + 1) * 2 : nullptr;
     if (w.b_validate) {
       j.bad_slot = &w.ctr->bad_slot;
       j.slot_limit = w.cav.n_given;
@@ -2804,7 +2806,7 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
   if (timing_env && w.timing) {
     HIP_OK(hipDeviceSynchronize());  // (a closure join publishes its batch before its last waves end)
     const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2;
-    const size_t cj_words = (size_t)kCjTimingWords * (n / 64 + 1);
+    const size_t cj_words = std::max((size_t)kCjTimingWords * (n / 64 + 1), (size_t)kLjTimingWords * (n / 16 + 1));
     std::vector<unsigned long long> h(timing_words + cj_words);
     HIP_OK(hipMemcpy(h.data(), w.timing, (timing_words + cj_words) * 8, hipMemcpyDeviceToHost));
     std::string path = std::string(timing_env) + ".bin";
@@ -2814,7 +2816,16 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
       fwrite(h.data(), 8, timing_words, f);
       fclose(f);
     }
-    if (w.b_closure) {  // the closure join's per-wave records: <prefix>_cj.bin
+    if (w.b_label) {  // the label join's per-wave records: <prefix>_lj.bin
+      std::string lpath = std::string(timing_env) + "_lj.bin";
+      if (FILE* f = fopen(lpath.c_str(), "ab")) {
+        const unsigned long long waves = (n + 31) / 32;
+        unsigned long long hdr[2] = {0x1AB0ull, waves};
+        fwrite(hdr, 8, 2, f);
+        fwrite(h.data() + timing_words, 8, (size_t)kLjTimingWords * waves, f);
+        fclose(f);
+      }
+    } else if (w.b_closure) {  // the closure join's per-wave records: <prefix>_cj.bin
       std::string cpath = std::string(timing_env) + "_cj.bin";
       if (FILE* f = fopen(cpath.c_str(), "ab")) {
         unsigned long long hdr[2] = {0xC10Cull, (n + 63) / 64};
