@@ -6,7 +6,8 @@ import sys
 import numpy as np
 
 TICK_US = 0.01
-W = 7  # labels.inc kLjTimingWords: start, items + table staged, slot lines staged, decided, end, list / ext checks
+W = 11  # labels.inc kLjTimingWords: start, items + table staged, slot lines staged, decided, end, list / ext checks,
+#        deferred: no root / slot overflow / dirty without overlay / overlay hit
 
 
 def launches(path):
@@ -34,7 +35,8 @@ def main(path):
         spans.append((r[:, 4].max() - t0) * TICK_US)
         recs.append(np.column_stack([(r[:, 0] - t0) * TICK_US, (r[:, 1] - r[:, 0]) * TICK_US,
                                      (r[:, 2] - r[:, 1]) * TICK_US, (r[:, 3] - r[:, 2]) * TICK_US,
-                                     (r[:, 4] - r[:, 3]) * TICK_US, (r[:, 4] - t0) * TICK_US, r[:, 5], r[:, 6]]))
+                                     (r[:, 4] - r[:, 3]) * TICK_US, (r[:, 4] - t0) * TICK_US, r[:, 5], r[:, 6],
+                                     r[:, 7], r[:, 8], r[:, 9], r[:, 10]]))
     a = np.concatenate(recs)
     print(f"launches {len(spans)}  span us (first wave start -> last wave end): {pct(np.array(spans))}")
     names = ["start offset", "items + table", "slot lines", "decide", "results + summary", "wave end offset"]
@@ -49,6 +51,9 @@ def main(path):
     slow = a[:, 5] >= np.percentile(a[:, 5], 99)
     print(f"slowest 1 % of waves: list checks {nl[slow].mean():.2f} ext checks {ne[slow].mean():.2f} "
           f"(all waves: {nl.mean():.2f} / {ne.mean():.2f})")
+    n_launch = max(1, len(spans))
+    print("deferred checks per launch: no label root %.1f, slot overflow %.1f, dirty subject (no overlay) %.1f, "
+          "overlay hit %.1f" % tuple(a[:, 8 + k].sum() / n_launch for k in range(4)))
 
 
 if __name__ == "__main__":
