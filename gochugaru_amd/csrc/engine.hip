@@ -1825,7 +1825,9 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
   return ds;
 }
 
-static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& adopted) {
+// sync_null false (a Watch publication, delta.inc device_apply_publish): the null stream's work is
+// not waited for here — its readers are ordered behind the publication's event
+static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& adopted, bool sync_null) {
   PhaseClock pc("publish");
   if (!ds->slot_patches.empty()) {  // (the batches in flight on the current snapshot have finished)
     for (const SlotPatch& sp : ds->slot_patches)
@@ -1874,6 +1876,7 @@ static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& ad
       free_list(e.dev->allocs);
     }
     pc.mark(n_free > 16 ? "free_many" : "free_few");
+    if (!sync_null && !e.dev->hallocs.empty()) spin_stream(e, nullptr);  // (the build's kernels may read them)
     for (void* p : e.dev->hallocs) (void)hipFree(p);
     pc.mark(e.dev->hallocs.empty() ? "free_h0" : "free_h");
     delete e.dev;
@@ -1882,14 +1885,16 @@ static void device_publish(Engine& e, DeviceSnapshot* ds, std::vector<void*>& ad
   e.dev = ds;
   static std::atomic<uint64_t> g_generations{0};  // process-wide: a snapshot id never repeats
   e.generation = ++g_generations;
-  HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
-  pc.mark("sync");
+  if (sync_null) {
+    HIP_OK(hipStreamSynchronize(nullptr));  // pool allocations are ordered on the null stream
+    pc.mark("sync");
+  }
 }
 
 void device_upload(Engine& e, std::vector<HostCSR>& csrs, bool delta) {
   std::vector<void*> adopted;
   DeviceSnapshot* ds = device_build(e, csrs, delta, adopted);
-  device_publish(e, ds, adopted);
+  device_publish(e, ds, adopted, true);
 }
 
 // ---- workspaces ------------------------------------------------------------------------------
@@ -2079,10 +2084,10 @@ void release_ws(Engine& e, Workspace* w) {
   e.ws_cv.notify_all();  // a two-workspace caller may be waiting beside one-workspace callers
 }
 
-// A Watch batch's membership-index patch runs on the null stream after its publication, not
-// waited for (delta.inc device_apply_publish): every launch that may probe the indexes — the wave
-// bundles, the level loop, the lookups; the joins do not — is ordered after it on the GPU by its
-// stream waiting for the patch's event (once per workspace, stream and patch).
+// A Watch publication's null-stream work — the merge, the label tables, the membership-index
+// patch — is not waited for (delta.inc device_apply_publish): every launch on the new snapshot is
+// ordered after it on the GPU by its stream waiting for the publication's event (once per
+// workspace, stream and publication).
 static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us, hipStream_t st) {
   if (e.patch_seq && (w.patch_seen != e.patch_seq || w.patch_stream != (void*)st)) {
     HIP_OK(hipStreamWaitEvent(st, (hipEvent_t)e.patch_ev, 0));
@@ -2483,6 +2488,13 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     if (!aql_ok) return false;
     const AqlKernel* k = aql_kernel(e.aql, name);
     if (!k) return false;
+    // (the HSA queues do not see the HIP streams' order: a Watch publication's null-stream work
+    // completes before the first dispatch on its snapshot; delta.inc device_apply_publish)
+    const uint64_t ps = e.patch_seq;
+    if (ps && e.aql_patch_seen.load(std::memory_order_acquire) != ps) {
+      spin_event((hipEvent_t)e.patch_ev);
+      e.aql_patch_seen.store(ps, std::memory_order_release);
+    }
     aql_dispatch(*e.aql, w, *k, args, bytes, blocks, w.b_timed);
     w.b_aql = true;
     return true;

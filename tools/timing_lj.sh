@@ -8,4 +8,6 @@ GCK_LIBRARY=$PWD/gochugaru_amd/libgck_timing.so GCK_DEBUG_TIMING=$OUT/t timeout 
   python bench.py --steps 10 --warmup 2 --no-cpu --no-oracle --host-steps 0 --inflight 1 "$@" > "$OUT/t.json" 2> "$OUT/t.err"
 python tools/analyze_lj.py "$OUT/t_lj.bin" > "$OUT/lj.txt"
 cat "$OUT/lj.txt"
+# (the bundles the join left, when any ran: tools/analyze_timing.py)
+if [ -s "$OUT/t.bin" ]; then python tools/analyze_timing.py "$OUT/t.bin" > "$OUT/bundles.txt" && cat "$OUT/bundles.txt"; fi
 rm -f "$OUT/t.bin" "$OUT/t_lj.bin" "$OUT/t_cj.bin"
