@@ -243,8 +243,10 @@ struct Workspace {
   DevCounters* h_ctr = nullptr;  // pinned, coherent (k_publish writes it)
   unsigned* h_seq = nullptr;     // after h_ctr + bundle counters: the last published batch
   unsigned pub_seq = 0;
-  uint64_t patch_seen = 0;       // the engine's index-patch sequence this workspace's stream waited for
+  uint64_t patch_seen = 0;       // the engine's publication whose patch event this workspace's stream waited for
   void* patch_stream = nullptr;  // ... on this stream (make_ctx)
+  uint64_t build_seen = 0;       // ... whose build event (the joins' wait)
+  void* build_stream = nullptr;
   unsigned* d_hpub = nullptr;    // device address of h_ctr
   unsigned* h_slots = nullptr;   // pinned: {deferred, counters touched} per block of an AQL-dispatched join
   unsigned* d_slots = nullptr;   // (device address)
@@ -1429,6 +1431,9 @@ int device_init(Engine& e) {
   hipEvent_t pev = nullptr;
   HIP_OK(hipEventCreateWithFlags(&pev, hipEventDisableTiming));
   e.patch_ev = pev;
+  hipEvent_t bev = nullptr;
+  HIP_OK(hipEventCreateWithFlags(&bev, hipEventDisableTiming));
+  e.build_ev = bev;
   e.device_ready = true;
   return 0;
 }
@@ -1532,6 +1537,8 @@ void device_free(Engine& e) {
     e.sync_ev = nullptr;
     if (e.patch_ev) (void)hipEventDestroy((hipEvent_t)e.patch_ev);
     e.patch_ev = nullptr;
+    if (e.build_ev) (void)hipEventDestroy((hipEvent_t)e.build_ev);
+    e.build_ev = nullptr;
     e.patch_seq = 0;
     if (e.blob_host) (void)hipHostFree(e.blob_host);
     e.blob_host = nullptr;
@@ -2087,12 +2094,24 @@ void release_ws(Engine& e, Workspace* w) {
 // A Watch publication's null-stream work — the merge, the label tables, the membership-index
 // patch — is not waited for (delta.inc device_apply_publish): every launch on the new snapshot is
 // ordered after it on the GPU by its stream waiting for the publication's event (once per
-// workspace, stream and publication).
-static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us, hipStream_t st) {
+// workspace, stream and publication). A join, which never probes the membership indexes, waits only
+// for the work before the index patch (probes = false); the launches after it that may probe them
+// wait for the patch too (wait_patch).
+static void wait_patch(Engine& e, Workspace& w, hipStream_t st) {
   if (e.patch_seq && (w.patch_seen != e.patch_seq || w.patch_stream != (void*)st)) {
     HIP_OK(hipStreamWaitEvent(st, (hipEvent_t)e.patch_ev, 0));
-    w.patch_seen = e.patch_seq;
-    w.patch_stream = (void*)st;
+    w.patch_seen = w.build_seen = e.patch_seq;
+    w.patch_stream = w.build_stream = (void*)st;
+  }
+}
+static Ctx make_ctx(Engine& e, Workspace& w, int64_t now_us, hipStream_t st, bool probes = true) {
+  if (probes) {
+    wait_patch(e, w, st);
+  } else if (e.patch_seq && (w.build_seen != e.patch_seq || w.build_stream != (void*)st) &&
+             (w.patch_seen != e.patch_seq || w.patch_stream != (void*)st)) {
+    HIP_OK(hipStreamWaitEvent(st, (hipEvent_t)e.build_ev, 0));
+    w.build_seen = e.patch_seq;
+    w.build_stream = (void*)st;
   }
   DeviceSnapshot& ds = *e.dev;
   Ctx c{};
@@ -2429,7 +2448,7 @@ static void aql_collect(Workspace& w) {
 
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
-  Ctx c = make_ctx(e, w, now_us, st);
+  Ctx c = make_ctx(e, w, now_us, st, false);  // (the bundles below wait for the index patch: wait_patch)
   c.ck_items = d_items;
   BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
   static const char* timing_env = getenv("GCK_DEBUG_TIMING");
@@ -2489,10 +2508,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     const AqlKernel* k = aql_kernel(e.aql, name);
     if (!k) return false;
     // (the HSA queues do not see the HIP streams' order: a Watch publication's null-stream work
-    // completes before the first dispatch on its snapshot; delta.inc device_apply_publish)
+    // before its index patch completes before the first join dispatched on its snapshot;
+    // delta.inc device_apply_publish)
     const uint64_t ps = e.patch_seq;
     if (ps && e.aql_patch_seen.load(std::memory_order_acquire) != ps) {
-      spin_event((hipEvent_t)e.patch_ev);
+      spin_event((hipEvent_t)e.build_ev);
       e.aql_patch_seen.store(ps, std::memory_order_release);
     }
     aql_dispatch(*e.aql, w, *k, args, bytes, blocks, w.b_timed);
@@ -2551,6 +2571,9 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     const AqlKernel* ak = aql_ok ? aql_kernel(e.aql, lj_names[v]) : nullptr;
     if (cav && ak) {
       j.cx = static_cast<const Ctx*>(aql_extra(w));  // (written with the arguments)
+    } else if (cav && e.aql && w.aql_kernarg && w.aql_devargs) {
+      aql_put_extra(*e.aql, w, &c, sizeof(Ctx));  // (through the BAR into VRAM: no copy on the stream)
+      j.cx = static_cast<const Ctx*>(aql_extra(w));
     } else if (cav) {
       *w.h_ctx = c;
       HIP_OK(hipMemcpyAsync(w.d_ctx, w.h_ctx, sizeof(Ctx), hipMemcpyHostToDevice, st));
@@ -2627,6 +2650,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       hipExtLaunchKernelGGL((k_closure_join<32, kCjLdsBytes>), grid, block, 0, st, e0, e1, 0, c, j);
     HIP_OK(hipGetLastError());
   } else {
+    wait_patch(e, w, st);
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev0, st));
     launch_wave_bundles(e, w, c, a, st);
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
@@ -2635,6 +2659,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     BundleArgs b = a;
     b.idx = w.c_deferred;
     b.n_dev = w.b_ctrs + 4;
+    wait_patch(e, w, st);
     launch_wave_bundles(e, w, c, b, st);
     if (w.b_timed) HIP_OK(hipEventRecord(w.ev1, st));
   }

@@ -219,8 +219,9 @@ struct Engine {
   void* delta_ev = nullptr;       // hipEvent_t: a Watch batch's merge totals are back (delta.inc)
   void* sync_ev = nullptr;        // hipEvent_t: the Watch path's polled waits (engine.hip spin_stream)
   void* patch_ev = nullptr;       // hipEvent_t: the last Watch publication's null-stream work, index patch included (make_ctx)
+  void* build_ev = nullptr;       // hipEvent_t: the same publication's work before its index patch (the joins wait for it)
   uint64_t patch_seq = 0;         // publications recorded (0: none yet)
-  std::atomic<uint64_t> aql_patch_seen{0};  // the publication the HSA-queue dispatches have waited for
+  std::atomic<uint64_t> aql_patch_seen{0};  // the publication whose build the HSA-queue dispatches have waited for
   void* blob_host = nullptr;      // pinned: a Watch batch's program upload (device_build)
   size_t blob_host_cap = 0;
   size_t delta_scratch_cap = 0;
