@@ -1502,6 +1502,7 @@ void device_free(Engine& e) {
   if (e.delta_host) {
     (void)hipHostFree(e.delta_host);
     e.delta_host = nullptr;
+    e.delta_host_dev = nullptr;
     e.delta_host_cap = 0;
   }
   if (e.dev) {

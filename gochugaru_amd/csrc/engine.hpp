@@ -227,6 +227,7 @@ struct Engine {
   size_t delta_scratch_cap = 0;
   void* delta_host = nullptr;     // pinned staging of the same (one upload, one small read back)
   size_t delta_host_cap = 0;
+  void* delta_host_dev = nullptr; // (its device address: the prefix writes the batch's totals there)
   GroupBuffers group_buf;  // group_updates' records and groups, kept across Watch batches
   // bumped by every write that can invalidate a batch validated earlier (a schema, a snapshot file,
   // an interner rollback, a partition): a staged Watch batch (gck_watch_stage) is regrouped at
