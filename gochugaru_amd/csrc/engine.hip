@@ -2447,6 +2447,17 @@ static void aql_collect(Workspace& w) {
   w.h_bctrs[4] = deferred;
 }
 
+// The HSA queues do not see the HIP streams' order: a Watch publication's null-stream work (merge,
+// label-table marks, program upload; delta.inc device_apply_build) completes before the first join
+// dispatched into a queue on its snapshot. Every aql_dispatch of a check batch comes through here.
+static void aql_after_build(Engine& e) {
+  const uint64_t ps = e.patch_seq;
+  if (ps && e.aql_patch_seen.load(std::memory_order_acquire) != ps) {
+    spin_event((hipEvent_t)e.build_ev);
+    e.aql_patch_seen.store(ps, std::memory_order_release);
+  }
+}
+
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   Ctx c = make_ctx(e, w, now_us, st, false);  // (the bundles below wait for the index patch: wait_patch)
@@ -2508,14 +2519,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     if (!aql_ok) return false;
     const AqlKernel* k = aql_kernel(e.aql, name);
     if (!k) return false;
-    // (the HSA queues do not see the HIP streams' order: a Watch publication's null-stream work
-    // before its index patch completes before the first join dispatched on its snapshot;
-    // delta.inc device_apply_publish)
-    const uint64_t ps = e.patch_seq;
-    if (ps && e.aql_patch_seen.load(std::memory_order_acquire) != ps) {
-      spin_event((hipEvent_t)e.build_ev);
-      e.aql_patch_seen.store(ps, std::memory_order_release);
-    }
+    aql_after_build(e);
     aql_dispatch(*e.aql, w, *k, args, bytes, blocks, w.b_timed);
     w.b_aql = true;
     return true;
@@ -2583,6 +2587,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     if (ak) {
       const uint32_t blocks = (n + 32u * kWaves - 1) / (32u * kWaves);
       if (j.h_out) aql_summaries(w, j.coherent, j.h_out, j.done, j.n_deferred, blocks);
+      aql_after_build(e);
       aql_dispatch(*e.aql, w, *ak, &j, sizeof(j), blocks, w.b_timed,
                    cav ? &c : nullptr, cav ? sizeof(Ctx) : 0);
       w.b_aql = true;
@@ -3072,7 +3077,8 @@ static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_
   w.b_copy_err = nullptr;
   w.b_validate = false;
   const bool join = label_join_on(e) || (e.dev->d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE));
-  if (host && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & GCK_FLAG_PROFILE) && join) {
+  if (host && e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & (GCK_FLAG_PROFILE | GCK_FLAG_NO_BUNDLE)) &&
+      join) {
     // the join reads every item once, in place: it also checks the context slots (no host pass
     // over the items on the submitting thread)
     w.b_validate = true;
@@ -3247,33 +3253,52 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
   if (ws[1] != ws[0]) g1.reset(new std::lock_guard<std::mutex>(ws[1]->m));
   stage_caveats(*ws[0], CavCall(cav), ws[0]->stream);
   if (ws[1] != ws[0]) stage_caveats(*ws[1], CavCall(cav), ws[1]->stream);
+  // several chunks: the context slots are checked here, before any GPU work, so that a bad item
+  // fails the call with its request index and no chunk is left writing the caller's buffers (a
+  // single chunk's zero-copy join checks its own items in place)
+  if (n_chunks > 1) validate_slots(items, (uint32_t)n, ws[0]->cav.n_given);
   float ms = 0.f;
   Workspace* prev = nullptr;
-  for (size_t k = 0; k < n_chunks; ++k) {
-    Workspace& w = *ws[k & 1];
-    const size_t pos = k * mb;
-    const uint32_t len = (uint32_t)std::min(n - pos, mb);
-    if (prev == &w) {  // one workspace (a pool of one): the previous chunk completes first
-      finish_batch(e, w);
-      copy_out(w);
-      w.state = 0;
-      ms += w.b_ms;
-      prev = nullptr;
+  try {
+    for (size_t k = 0; k < n_chunks; ++k) {
+      Workspace& w = *ws[k & 1];
+      const size_t pos = k * mb;
+      const uint32_t len = (uint32_t)std::min(n - pos, mb);
+      if (prev == &w) {  // one workspace (a pool of one): the previous chunk completes first
+        finish_batch(e, w);
+        copy_out(w);
+        w.state = 0;
+        ms += w.b_ms;
+        prev = nullptr;
+      }
+      submit_batch(e, w, items + pos, len, now_us, perm + pos, err + pos, nullptr, true);
+      if (prev) {
+        finish_batch(e, *prev);
+        copy_out(*prev);
+        prev->state = 0;
+        ms += prev->b_ms;
+      }
+      prev = &w;
     }
-    submit_batch(e, w, items + pos, len, now_us, perm + pos, err + pos, nullptr, true);
     if (prev) {
       finish_batch(e, *prev);
       copy_out(*prev);
       prev->state = 0;
       ms += prev->b_ms;
     }
-    prev = &w;
-  }
-  if (prev) {
-    finish_batch(e, *prev);
-    copy_out(*prev);
-    prev->state = 0;
-    ms += prev->b_ms;
+  } catch (...) {
+    // a chunk failed: every other chunk still in flight completes (its kernels end and its
+    // completion signal is consumed) before the workspaces go back to the pool
+    for (Workspace* x : {ws[0], ws[1]}) {
+      if (x->state == 1) {
+        try {
+          finish_batch(e, *x);
+        } catch (...) {
+        }
+      }
+      x->state = 0;
+    }
+    throw;
   }
   std::lock_guard<std::mutex> sl(e.stats_mu);
   e.stats.kernel_ms = ms;

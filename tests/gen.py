@@ -426,6 +426,56 @@ def near_budget(seed, n_users=40, n_groups=48, n_folders=24, n_docs=40):
 GDOCS_NOWILD = GDOCS.replace("relation viewer: user | user:* | group#member", "relation viewer: user | group#member")
 
 
+HUB_ARROW = """
+definition user {
+  relation manager: user
+}
+definition org {
+  relation member: user
+  permission member_mgr = member->manager
+}
+definition repo {
+  relation org: org
+  relation reader: user
+  permission read = reader + org->member
+  permission audit = org->member_mgr
+}
+"""
+
+
+def hub_arrow(seed, n_users=60, n_orgs=10, n_repos=50):
+    """A hub relation (org#member: arrows point at it) whose rows are also read as an arrow's
+    tupleset outside the hub (org#member_mgr = member->manager). A partitioned graph keeps a hub's
+    direct tuples with their subjects' owners, so such a relation must not be a hub there
+    (labels.inc partition_rules)."""
+    rng = random.Random(seed)
+    t = []
+    for u in range(n_users):
+        if rng.random() < 0.6:
+            t.append(f"user:u{u}#manager@user:u{_pick(rng, n_users)}")
+    for o in range(n_orgs):
+        for _ in range(rng.randint(1, 6)):
+            t.append(f"org:o{o}#member@user:u{_pick(rng, n_users)}")
+    for r in range(n_repos):
+        if rng.random() < 0.9:
+            t.append(f"repo:r{r}#org@org:o{_pick(rng, n_orgs)}")
+        for _ in range(rng.randint(0, 2)):
+            t.append(f"repo:r{r}#reader@user:u{_pick(rng, n_users)}")
+    t = sorted(set(t))
+    checks = []
+    for _ in range(300):
+        x = rng.random()
+        if x < 0.35:
+            checks.append(f"repo:r{_pick(rng, n_repos)}#read@user:u{_pick(rng, n_users)}")
+        elif x < 0.65:
+            checks.append(f"repo:r{_pick(rng, n_repos)}#audit@user:u{_pick(rng, n_users)}")
+        elif x < 0.85:
+            checks.append(f"org:o{_pick(rng, n_orgs)}#member_mgr@user:u{_pick(rng, n_users)}")
+        else:
+            checks.append(f"org:o{_pick(rng, n_orgs)}#member@user:u{_pick(rng, n_users)}")
+    return HUB_ARROW, t, checks
+
+
 def check_contexts(seed, n):
     """Check-time caveat contexts for n checks (CheckBulkPermissionsRequestItem.Context):
     none, a satisfying one or a failing one for only_on_tuesday, and an unrelated key."""
@@ -435,7 +485,7 @@ def check_contexts(seed, n):
 
 
 FAMILIES = {"gdocs": gdocs, "github": github, "caveated": caveated, "nested": nested,
-            "gdocs_deep": gdocs_deep, "cyclic": cyclic, "near_budget": near_budget}
+            "gdocs_deep": gdocs_deep, "cyclic": cyclic, "near_budget": near_budget, "hub_arrow": hub_arrow}
 # the dispatch depth budget a family is checked under (default: SpiceDB's 50)
 FAMILY_DEPTH = {"near_budget": 8}
 NOW_US = 1759449600 * 1_000_000  # 2025-10-03T00:00:00Z

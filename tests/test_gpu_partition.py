@@ -125,7 +125,7 @@ def _run(tmp_path, world, family, seed, watch=False):
 
 
 FAMILIES = [("nested", 1), ("gdocs", 2), ("gdocs_deep", 3), ("github", 1), ("github", 4), ("cyclic", 2),
-            ("near_budget", 3), ("caveated", 2)]
+            ("near_budget", 3), ("caveated", 2), ("hub_arrow", 1)]
 
 
 @pytest.mark.parametrize("world", [2, 3])
