@@ -14,6 +14,9 @@
 using submit_fn = int (*)(gck_engine*, const gck_consistency*, const gck_item*, size_t, const char* const*,
                           const size_t*, size_t, int64_t, uint8_t*, int32_t*, uint32_t, void*, gck_batch**);
 using wait_fn = int (*)(gck_engine*, gck_batch*);
+using submit_uniform_fn = int (*)(gck_engine*, const gck_consistency*, const gck_uniform*, const uint32_t*, size_t,
+                                  const char* const*, const size_t*, size_t, int64_t, uint64_t*, gck_item_error*,
+                                  size_t, size_t*, gck_batch**);
 
 // Optional per-batch timeline of the next loops (gckd_set_trace): for batch k, the seconds after
 // the loop's start at which its submit and its wait returned (stamps[2k], stamps[2k + 1]).
@@ -87,6 +90,42 @@ int gckd_run_host(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consi
     gck_batch* b = nullptr;
     rc = submit(e, cs, reinterpret_cast<const gck_item*>(items[k]), n, nullptr, nullptr, 0, now_us,
                 reinterpret_cast<uint8_t*>(perm[k]), reinterpret_cast<int32_t*>(err[k]), 0u, nullptr, &b);
+    if (rc == GCK_OK) q.push_back(b);
+    stamp(t0, k, 0);
+  }
+  size_t kw = n_batches - q.size();
+  while (!q.empty()) {
+    const int r = wait(e, q.front());
+    stamp(t0, kw++, 1);
+    if (rc == GCK_OK) rc = r;
+    q.pop_front();
+  }
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+// The same loop over uniform requests (gck_check_submit_uniform): one header, host pairs[k] (n pairs
+// of u32 ids) in, packed[k] (ceil(n / 32) words) and errs[k] (err_cap records, the count in
+// n_errs[k]) out — what Client.Check sends for relationships of one shape, in 8 B per check.
+int gckd_run_uniform(submit_uniform_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs,
+                     const gck_uniform* hdr, size_t n_batches, const uint64_t* pairs, const uint64_t* packed,
+                     const uint64_t* errs, size_t err_cap, size_t* n_errs, size_t n, uint32_t depth, int64_t now_us,
+                     double* seconds) {
+  if (depth == 0) depth = 1;
+  std::deque<gck_batch*> q;
+  int rc = GCK_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t k = 0; k < n_batches && rc == GCK_OK; ++k) {
+    if (q.size() >= depth) {
+      rc = wait(e, q.front());
+      stamp(t0, k - depth, 1);
+      q.pop_front();
+      if (rc != GCK_OK) break;
+    }
+    gck_batch* b = nullptr;
+    rc = submit(e, cs, hdr, reinterpret_cast<const uint32_t*>(pairs[k]), n, nullptr, nullptr, 0, now_us,
+                reinterpret_cast<uint64_t*>(packed[k]), reinterpret_cast<gck_item_error*>(errs[k]), err_cap,
+                n_errs ? n_errs + k : nullptr, &b);
     if (rc == GCK_OK) q.push_back(b);
     stamp(t0, k, 0);
   }

@@ -221,6 +221,20 @@ struct Workspace {
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
   uint32_t b_sum_blocks = 0;  // ... in that many blocks, each with a summary slot (closure.inc block_summary)
   bool b_validate = false;    // host items read in place: the join checks their context slots
+  // ---- a uniform batch (gck_check_bulk_uniform / gck_check_submit_uniform) -----------------
+  bool u_on = false;          // this batch is uniform: its wait packs the results (uniform_collect)
+  bool u_join = false;        // ... and its join reads the pairs and writes the packed words in place
+  uint32_t u_rp = 0, u_ss = 0, u_ctx = 0;       // the header (closure.inc CjArgs::u_rp ...)
+  const uint32_t* u_pairs = nullptr;            // the pairs the join reads (caller's pinned buffer or staging)
+  unsigned long long* u_packed = nullptr;       // the words the join writes (caller's pinned buffer or staging)
+  unsigned long long* u_out = nullptr;          // the caller's words
+  uint32_t u_ncj = 0;                           // checks the join left (answered into d_perm / d_err)
+  std::vector<gck_item> u_items;                // otherwise: the request expanded to items ...
+  std::vector<uint8_t> u_perm;                  // ... and its results
+  std::vector<int32_t> u_err;
+  gck_item_error* u_errs = nullptr;             // submit_uniform: the caller's error list
+  size_t u_err_cap = 0;
+  size_t* u_n_errs = nullptr;
   void* aql_kernarg = nullptr;  // aql.inc: kernarg block of the dispatched join (pinned host memory, or VRAM)
   bool aql_devargs = false;     // ... in VRAM (aql.inc AqlState::devargs)
   uint64_t aql_signal = 0;      // aql.inc: its completion signal (hsa_signal_t handle)
@@ -2447,6 +2461,20 @@ static void aql_collect(Workspace& w) {
   w.h_bctrs[4] = deferred;
 }
 
+// A uniform batch's join arguments (closure.inc CjArgs::pairs; labels.inc LjArgs): the pairs and
+// the header in, the packed words out, and the items of the checks it leaves to the bundle stages
+// written where those read them (the workspace's item array, which the batch runs on).
+template <typename Args>
+static void uniform_args(const Workspace& w, Args& j) {
+  j.pairs = w.u_pairs;
+  j.out_packed = w.u_packed;
+  j.items_out = const_cast<gck_item*>(w.b_items);
+  j.u_rp = w.u_rp;
+  j.u_ss = w.u_ss;
+  j.u_ctx = w.u_ctx;
+  j.items = nullptr;
+}
+
 // The HSA queues do not see the HIP streams' order: a Watch publication's null-stream work (merge,
 // label-table marks, program upload; delta.inc device_apply_build) completes before the first join
 // dispatched into a queue on its snapshot. Every aql_dispatch of a check batch comes through here.
@@ -2555,6 +2583,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.bad_slot = &w.ctr->bad_slot;
       j.slot_limit = w.cav.n_given;
     }
+    if (w.u_join) uniform_args(w, j);
     if (self_pub) {  // self-published (see the closure join below)
       j.pub = reinterpret_cast<unsigned*>(w.ctr);
       j.pub_words = kPubWords;
@@ -2614,6 +2643,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
       j.bad_slot = &w.ctr->bad_slot;
       j.slot_limit = w.cav.n_given;
     }
+    if (w.u_join) uniform_args(w, j);
     // self-published as the label join (a host-side stream query or synchronisation per batch
     // instead costs ~10 us, 11 G -> 3-5 G checks/s)
     if (self_pub) {
@@ -2699,6 +2729,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
   bm = ms;
   const uint32_t n_cj = w.b_closure ? w.h_bctrs[4] : 0u;
   if (n_cj > n) throw Error(GCK_E_DEVICE, "engine invariant violated: closure-join deferred count");
+  w.u_ncj = n_cj;
   if (w.b_closure) {
     // the join counts only its task-round checks (DevCounters::closure; usually none, so usually
     // no atomic): the rest of what it answered came from the slots
@@ -3054,7 +3085,9 @@ void host_free_all(Engine& e) {
 }
 
 static void submit_batch(Engine& e, Workspace& w, const gck_item* items, uint32_t n, int64_t now_us, uint8_t* perm,
-                         int32_t* err, hipStream_t st, bool host, bool own_stream = false) {
+                         int32_t* err, hipStream_t st, bool host, bool own_stream = false, bool uniform_join = false) {
+  w.u_join = uniform_join;  // (the join's arguments: bundles_launch)
+  w.u_on = false;           // (submit_uniform sets it after this)
   w.b_own_stream = own_stream;
   w.b_n = n;
   w.b_now = now_us;
@@ -3315,6 +3348,169 @@ void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int
   submit_batch(e, *w, items, (uint32_t)n, now_us, perm, err, st, host, !host && engine_stream);
 }
 
+// ---- uniform batches (include/gck.h gck_check_bulk_uniform, gck_check_submit_uniform) ----------
+// One header and (resource id, subject id) pairs in, 2-bit results out. With a one-round join on
+// the engine's queues the join reads the pairs and writes the packed words in place (zero-copy:
+// 8 B per check in, 1/4 B out across PCIe) and writes the item of each check it leaves into the
+// workspace's item array, where the bundle stages answer it; the wait patches those into the words
+// and lists the errors. Otherwise the request is expanded to items and runs as a host batch.
+static void submit_uniform(Engine& e, Workspace& w, const gck_uniform& h, const uint32_t* pairs, uint32_t n,
+                           int64_t now_us, unsigned long long* packed) {
+  const uint32_t rp = (uint32_t)h.resource_type | (uint32_t)h.permission << 16;
+  const uint32_t ss = (uint32_t)h.subject_type | (uint32_t)h.subject_relation << 16;
+  const bool join = label_join_on(e) || (e.dev->d_cj && !(e.cfg.flags & GCK_FLAG_NO_CLOSURE));
+  if (e.aql && w.aql_kernarg && !w.cav_on && !(e.cfg.flags & (GCK_FLAG_PROFILE | GCK_FLAG_NO_BUNDLE)) && join) {
+    const size_t words = ((size_t)n + 31u) / 32u;
+    const bool pin_in = host_pinned(e, pairs, (size_t)n * 8u), pin_out = host_pinned(e, packed, words * 8u);
+    if (!pin_in) std::memcpy(w.h_items, pairs, (size_t)n * 8u);
+    w.u_rp = rp;
+    w.u_ss = ss;
+    w.u_ctx = h.context_slot;
+    w.u_pairs = pin_in ? pairs : reinterpret_cast<const uint32_t*>(w.h_items);
+    // (the staging's result region holds 4 B per check: room for the words)
+    w.u_packed = pin_out ? packed : reinterpret_cast<unsigned long long*>(w.h_err);
+    submit_batch(e, w, w.d_items, n, now_us, w.d_perm, w.d_err, w.stream, false, true, true);
+  } else {
+    w.u_items.resize(n);
+    for (uint32_t k = 0; k < n; ++k) {
+      gck_item& it = w.u_items[k];
+      it.resource_type = h.resource_type;
+      it.permission = h.permission;
+      it.resource_id = pairs[2 * (size_t)k];
+      it.subject_type = h.subject_type;
+      it.subject_relation = h.subject_relation;
+      it.subject_id = pairs[2 * (size_t)k + 1];
+      it.context_slot = h.context_slot;
+    }
+    w.u_perm.resize(n);
+    w.u_err.resize(n);
+    w.u_packed = nullptr;
+    submit_batch(e, w, w.u_items.data(), n, now_us, w.u_perm.data(), w.u_err.data(), nullptr, true);
+  }
+  w.u_on = true;
+  w.u_out = packed;
+  w.u_ncj = 0;
+}
+
+// After a uniform batch has finished (finish_batch, copy_out): its words into the caller's buffer
+// and its errors, at request offset `pos`, appended to `errs`.
+static void uniform_collect(Workspace& w, uint32_t pos, std::vector<gck_item_error>& errs) {
+  const uint32_t n = w.b_n;
+  const size_t words = ((size_t)n + 31u) / 32u;
+  if (w.u_join) {
+    unsigned long long* out = w.u_packed;
+    if (w.u_ncj) {  // the checks the join left: their results from the bundle stages
+      std::vector<uint32_t> idx(w.u_ncj);
+      w.u_perm.resize(n);
+      w.u_err.resize(n);
+      HIP_OK(hipMemcpyAsync(idx.data(), w.c_deferred, idx.size() * 4u, hipMemcpyDeviceToHost, w.stream));
+      HIP_OK(hipMemcpyAsync(w.u_perm.data(), w.d_perm, n, hipMemcpyDeviceToHost, w.stream));
+      HIP_OK(hipMemcpyAsync(w.u_err.data(), w.d_err, (size_t)n * 4u, hipMemcpyDeviceToHost, w.stream));
+      HIP_OK(hipStreamSynchronize(w.stream));
+      for (uint32_t i : idx) {
+        if (i >= n) throw Error(GCK_E_DEVICE, "engine invariant violated: deferred index");
+        if (w.u_err[i]) errs.push_back(gck_item_error{pos + i, w.u_err[i]});
+        else out[i >> 5] |= (unsigned long long)(w.u_perm[i] & 3u) << (2u * (i & 31u));
+      }
+    }
+    if (out != w.u_out) std::memcpy(w.u_out, out, words * 8u);
+  } else {
+    for (size_t k = 0; k < words; ++k) {
+      unsigned long long x = 0;
+      const uint32_t b = (uint32_t)k * 32u, m = std::min<uint32_t>(32u, n - b);
+      for (uint32_t q = 0; q < m; ++q) {
+        const uint32_t i = b + q;
+        if (w.u_err[i]) errs.push_back(gck_item_error{pos + i, w.u_err[i]});
+        else x |= (unsigned long long)(w.u_perm[i] & 3u) << (2u * q);
+      }
+      w.u_out[k] = x;
+    }
+  }
+}
+
+static void uniform_errors(std::vector<gck_item_error>& errs, gck_item_error* out, size_t cap, size_t* n_errs) {
+  std::sort(errs.begin(), errs.end(),
+            [](const gck_item_error& x, const gck_item_error& y) { return x.index < y.index; });
+  const size_t m = std::min(cap, errs.size());
+  if (m && out) std::memcpy(out, errs.data(), m * sizeof(gck_item_error));
+  if (n_errs) *n_errs = errs.size();
+}
+
+void device_submit_uniform(Engine& e, Workspace* w, const gck_uniform& h, const uint32_t* pairs, size_t n,
+                           int64_t now_us, uint64_t* packed, gck_item_error* errs, size_t cap, size_t* n_errs,
+                           CavCall cav) {
+  HIP_OK(hipSetDevice(e.device));
+  std::lock_guard<std::mutex> lk(w->m);
+  if (n > w->max_batch) throw Error(GCK_E_INVALID_ARGUMENT, "submitted batch above max_batch");
+  stage_caveats(*w, std::move(cav), w->stream);
+  if (now_us == 0) now_us = wall_now_us();
+  submit_uniform(e, *w, h, pairs, (uint32_t)n, now_us, reinterpret_cast<unsigned long long*>(packed));
+  w->u_errs = errs;
+  w->u_err_cap = cap;
+  w->u_n_errs = n_errs;
+}
+
+// Synchronous: chunks of max_batch (a multiple of 32 checks, so that each chunk's words start a
+// word) on two workspaces in turn, as device_check_host.
+void device_check_uniform(Engine& e, Workspace* w0, Workspace* w1, const gck_uniform& h, const uint32_t* pairs,
+                          size_t n, int64_t now_us, uint64_t* packed, gck_item_error* out_errs, size_t cap,
+                          size_t* n_errs, const CavCall& cav) {
+  HIP_OK(hipSetDevice(e.device));
+  if (now_us == 0) now_us = wall_now_us();
+  const size_t mb = w0->max_batch >= 32 ? (w0->max_batch & ~(size_t)31) : w0->max_batch;
+  if (n > mb && mb % 32 != 0) throw Error(GCK_E_CAPACITY, "a uniform request above max_batch needs max_batch >= 32");
+  const size_t n_chunks = (n + mb - 1) / mb;
+  Workspace* ws[2] = {w0, (w1 && n_chunks > 1) ? w1 : w0};
+  std::lock_guard<std::mutex> g0(ws[0]->m);
+  std::unique_ptr<std::lock_guard<std::mutex>> g1;
+  if (ws[1] != ws[0]) g1.reset(new std::lock_guard<std::mutex>(ws[1]->m));
+  stage_caveats(*ws[0], CavCall(cav), ws[0]->stream);
+  if (ws[1] != ws[0]) stage_caveats(*ws[1], CavCall(cav), ws[1]->stream);
+  std::vector<gck_item_error> errs;
+  size_t pos_of[2] = {0, 0};
+  float ms = 0.f;
+  Workspace* prev = nullptr;
+  auto complete = [&](Workspace& w) {
+    finish_batch(e, w);
+    copy_out(w);
+    uniform_collect(w, (uint32_t)pos_of[&w == ws[0] ? 0 : 1], errs);
+    w.state = 0;
+    w.u_on = false;
+    ms += w.b_ms;
+  };
+  try {
+    for (size_t k = 0; k < n_chunks; ++k) {
+      Workspace& w = *ws[k & 1];
+      const size_t pos = k * mb;
+      const uint32_t len = (uint32_t)std::min(n - pos, mb);
+      if (prev == &w) {
+        complete(w);
+        prev = nullptr;
+      }
+      pos_of[&w == ws[0] ? 0 : 1] = pos;
+      submit_uniform(e, w, h, pairs + 2 * pos, len, now_us, reinterpret_cast<unsigned long long*>(packed + pos / 32));
+      if (prev) complete(*prev);
+      prev = &w;
+    }
+    if (prev) complete(*prev);
+  } catch (...) {
+    for (Workspace* x : {ws[0], ws[1]}) {
+      if (x->state == 1) {
+        try {
+          finish_batch(e, *x);
+        } catch (...) {
+        }
+      }
+      x->state = 0;
+      x->u_on = false;
+    }
+    throw;
+  }
+  uniform_errors(errs, out_errs, cap, n_errs);
+  std::lock_guard<std::mutex> sl(e.stats_mu);
+  e.stats.kernel_ms = ms;
+}
+
 // Completes a submitted batch. Takes no engine lock: a writer that wants to replace the
 // snapshot finishes the batch first (drain_batches, under w->m), so the snapshot cannot change
 // while this runs the later stages.
@@ -3323,8 +3519,15 @@ void device_wait(Engine& e, Workspace* w) {
   std::lock_guard<std::mutex> lk(w->m);
   finish_batch(e, *w);  // no-op when a writer already finished it (drain_batches)
   w->state = 0;
+  const bool uni = w->u_on;
+  w->u_on = false;
   if (w->fail_code) throw Error(w->fail_code, w->fail_msg);
   copy_out(*w);
+  if (uni) {
+    std::vector<gck_item_error> errs;
+    uniform_collect(*w, 0, errs);
+    uniform_errors(errs, w->u_errs, w->u_err_cap, w->u_n_errs);
+  }
   std::lock_guard<std::mutex> sl(e.stats_mu);
   e.stats.kernel_ms = w->b_ms;
 }

@@ -351,6 +351,15 @@ void device_check_host(Engine& e, Workspace* w0, Workspace* w1, const gck_item* 
 void device_submit(Engine& e, Workspace* w, const gck_item* items, size_t n, int64_t now_us, uint8_t* perm,
                    int32_t* err, void* stream, bool host, bool engine_stream, CavCall cav);
 void device_wait(Engine& e, Workspace* w);
+// Uniform requests (gck_check_bulk_uniform / gck_check_submit_uniform): one header, id pairs, packed
+// 2-bit results and the errored checks' (index, code) records in ascending order (the first `cap`
+// written, their number in *n_errs). The submitted form's outputs are written by device_wait.
+void device_check_uniform(Engine& e, Workspace* w0, Workspace* w1, const gck_uniform& h, const uint32_t* pairs,
+                          size_t n, int64_t now_us, uint64_t* packed, gck_item_error* errs, size_t cap,
+                          size_t* n_errs, const CavCall& cav);
+void device_submit_uniform(Engine& e, Workspace* w, const gck_uniform& h, const uint32_t* pairs, size_t n,
+                           int64_t now_us, uint64_t* packed, gck_item_error* errs, size_t cap, size_t* n_errs,
+                           CavCall cav);
 // Pinned host buffers (gck_host_alloc): a host batch whose items / results live in one is
 // copied by DMA directly, without the workspace's staging copy.
 void* host_alloc(Engine& e, size_t bytes);

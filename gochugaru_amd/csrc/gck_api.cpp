@@ -928,15 +928,16 @@ static void check_request(Engine& e, const gck_consistency* cs, const gck_item* 
   (void)host_items;
 }
 
-int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
-                       const char* const* contexts, const size_t* context_lens, size_t n_contexts,
-                       int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
+int gck_check_bulk_at(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                      const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                      int64_t now_us, uint8_t* out_perm, int32_t* out_err, uint64_t* out_revision) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(n == 0 || (items && out_perm && out_err), GCK_E_INVALID_ARGUMENT, "null buffers");
     if (n == 0) {  // empty request -> empty response (client/client_test.go:203-207)
       std::shared_lock<std::shared_mutex> lk(e.mu);
       check_request(e, cs, items, 0, true, contexts, context_lens, n_contexts);
+      if (out_revision) *out_revision = e.revision;
       return;
     }
     // workspaces first, then the engine lock (engine.hpp WsLease)
@@ -954,16 +955,72 @@ int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item
         if (ws[1] && ws[1] != ws[0]) release_ws(e, ws[1]);
       }
     } rel{e, ws};
+    // (the shared lock is held until the results are written: no Watch batch publishes meanwhile,
+    // so the revision read here is the one every chunk runs on)
     std::shared_lock<std::shared_mutex> lk(e.mu);
     check_request(e, cs, items, n, true, contexts, context_lens, n_contexts);
     const CavCall cav = caveat_call(e, contexts, context_lens, n_contexts);
+    const uint64_t rev = e.revision;
     device_check_host(e, ws[0], ws[1], items, n, now_us, out_perm, out_err, cav);
+    if (out_revision) *out_revision = rev;
   });
+}
+
+int gck_check_bulk_ctx(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
+                       const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                       int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
+  return gck_check_bulk_at(ge, cs, items, n, contexts, context_lens, n_contexts, now_us, out_perm, out_err, nullptr);
 }
 
 int gck_check_bulk(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
                    int64_t now_us, uint8_t* out_perm, int32_t* out_err) {
-  return gck_check_bulk_ctx(ge, cs, items, n, nullptr, nullptr, 0, now_us, out_perm, out_err);
+  return gck_check_bulk_at(ge, cs, items, n, nullptr, nullptr, 0, now_us, out_perm, out_err, nullptr);
+}
+
+// A uniform request's header against the call (include/gck.h gck_uniform): its context slot is
+// every pair's, so it is checked once here.
+static void check_uniform(const gck_uniform* h, size_t n_contexts) {
+  REQUIRE(h, GCK_E_INVALID_ARGUMENT, "null header");
+  REQUIRE(h->context_slot <= n_contexts, GCK_E_INVALID_ARGUMENT,
+          "uniform header: context_slot " + std::to_string(h->context_slot) + " beyond the " +
+              std::to_string(n_contexts) + " contexts given");
+}
+
+int gck_check_bulk_uniform(gck_engine* ge, const gck_consistency* cs, const gck_uniform* hdr, const uint32_t* pairs,
+                           size_t n, const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                           int64_t now_us, uint64_t* out_packed, gck_item_error* out_errs, size_t err_cap,
+                           size_t* out_n_errs, uint64_t* out_revision) {
+  return guard([&] {
+    Engine& e = need(ge);
+    check_uniform(hdr, n_contexts);
+    REQUIRE(n == 0 || (pairs && out_packed), GCK_E_INVALID_ARGUMENT, "null buffers");
+    REQUIRE(err_cap == 0 || out_errs, GCK_E_INVALID_ARGUMENT, "null error list");
+    if (out_n_errs) *out_n_errs = 0;
+    if (n == 0) {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      check_request(e, cs, nullptr, 0, true, contexts, context_lens, n_contexts);
+      if (out_revision) *out_revision = e.revision;
+      return;
+    }
+    precheck(e);
+    const size_t mb = e.cfg.max_batch ? e.cfg.max_batch : 65536;
+    Workspace* ws[2] = {nullptr, nullptr};
+    acquire_ws_n(e, n > (mb & ~(size_t)31) ? 2 : 1, ws);
+    struct Release {
+      Engine& e;
+      Workspace** ws;
+      ~Release() {
+        release_ws(e, ws[0]);
+        if (ws[1] && ws[1] != ws[0]) release_ws(e, ws[1]);
+      }
+    } rel{e, ws};
+    std::shared_lock<std::shared_mutex> lk(e.mu);
+    check_request(e, cs, nullptr, n, true, contexts, context_lens, n_contexts);
+    const CavCall cav = caveat_call(e, contexts, context_lens, n_contexts);
+    const uint64_t rev = e.revision;
+    device_check_uniform(e, ws[0], ws[1], *hdr, pairs, n, now_us, out_packed, out_errs, err_cap, out_n_errs, cav);
+    if (out_revision) *out_revision = rev;
+  });
 }
 
 int gck_check_bulk_device_ctx(gck_engine* ge, const gck_item* d_items, size_t n, const char* const* contexts,
@@ -995,6 +1052,7 @@ int gck_check_bulk_device(gck_engine* ge, const gck_item* d_items, size_t n, int
 // batch, nothing to do.
 struct gck_batch {
   Workspace* w = nullptr;
+  uint64_t revision = 0;  // the snapshot's revision at submit: the one the batch runs on
 };
 
 int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* items, size_t n,
@@ -1011,6 +1069,7 @@ int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* 
       std::shared_lock<std::shared_mutex> lk(e.mu);
       try {
         check_request(e, cs, items, 0, host, contexts, context_lens, n_contexts);
+        b->revision = e.revision;
       } catch (...) {
         delete b;
         throw;
@@ -1023,8 +1082,52 @@ int gck_check_submit(gck_engine* ge, const gck_consistency* cs, const gck_item* 
     try {
       std::shared_lock<std::shared_mutex> lk(e.mu);
       check_request(e, cs, items, n, host, contexts, context_lens, n_contexts);
+      b->revision = e.revision;
       device_submit(e, w, items, n, now_us, out_perm, out_err, stream, host, !host && (flags & GCK_SUBMIT_ENGINE_STREAM),
                     caveat_call(e, contexts, context_lens, n_contexts));
+    } catch (...) {
+      release_ws(e, w);
+      delete b;
+      throw;
+    }
+    b->w = w;
+    *out = b;
+  });
+}
+
+int gck_check_submit_uniform(gck_engine* ge, const gck_consistency* cs, const gck_uniform* hdr, const uint32_t* pairs,
+                             size_t n, const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                             int64_t now_us, uint64_t* out_packed, gck_item_error* out_errs, size_t err_cap,
+                             size_t* out_n_errs, gck_batch** out) {
+  return guard([&] {
+    Engine& e = need(ge);
+    REQUIRE(out, GCK_E_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    check_uniform(hdr, n_contexts);
+    REQUIRE(n == 0 || (pairs && out_packed), GCK_E_INVALID_ARGUMENT, "null buffers");
+    REQUIRE(err_cap == 0 || out_errs, GCK_E_INVALID_ARGUMENT, "null error list");
+    if (out_n_errs) *out_n_errs = 0;
+    auto* b = new gck_batch();
+    if (n == 0) {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      try {
+        check_request(e, cs, nullptr, 0, true, contexts, context_lens, n_contexts);
+        b->revision = e.revision;
+      } catch (...) {
+        delete b;
+        throw;
+      }
+      *out = b;
+      return;
+    }
+    precheck(e);
+    Workspace* w = acquire_ws(e);
+    try {
+      std::shared_lock<std::shared_mutex> lk(e.mu);
+      check_request(e, cs, nullptr, n, true, contexts, context_lens, n_contexts);
+      b->revision = e.revision;
+      device_submit_uniform(e, w, *hdr, pairs, n, now_us, out_packed, out_errs, err_cap, out_n_errs,
+                            caveat_call(e, contexts, context_lens, n_contexts));
     } catch (...) {
       release_ws(e, w);
       delete b;
@@ -1050,11 +1153,14 @@ int gck_host_free(gck_engine* ge, void* p) {
   });
 }
 
-int gck_check_wait(gck_engine* ge, gck_batch* b) {
+int gck_check_wait(gck_engine* ge, gck_batch* b) { return gck_check_wait_at(ge, b, nullptr); }
+
+int gck_check_wait_at(gck_engine* ge, gck_batch* b, uint64_t* out_revision) {
   return guard([&] {
     Engine& e = need(ge);
     REQUIRE(b, GCK_E_INVALID_ARGUMENT, "null batch");
     std::unique_ptr<gck_batch> own(b);
+    if (out_revision) *out_revision = b->revision;
     if (!b->w) return;
     Workspace* w = b->w;
     try {

@@ -130,6 +130,24 @@ class _Stats(C.Structure):
                 ("label_checks", C.c_uint64), ("aql_batches", C.c_uint64)]
 
 
+class Uniform(C.Structure):
+    """gck_uniform (include/gck.h): the shared shape of a uniform request's checks."""
+    _fields_ = [("resource_type", C.c_uint16), ("permission", C.c_uint16), ("subject_type", C.c_uint16),
+                ("subject_relation", C.c_uint16), ("context_slot", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+# gck_item_error: (index, GCK_ITEM_*) of a uniform request's errored checks
+ITEM_ERROR_DTYPE = np.dtype([("index", "<u4"), ("code", "<i4")])
+
+
+def unpack_results(words: np.ndarray, n: int) -> np.ndarray:
+    """The Permissionship of each of n checks from a uniform request's packed words (2 bits per
+    check, 32 per little-endian u64 word: include/gck.h gck_check_bulk_uniform)."""
+    b = np.ascontiguousarray(words, dtype="<u8").view(np.uint8)
+    four = np.stack([(b >> s) & 3 for s in (0, 2, 4, 6)], axis=1).reshape(-1)
+    return four[:n].astype(np.uint8)
+
+
 # symbol -> (restype, argtypes); the ABI test checks this list against include/gck.h
 _P = C.c_void_p
 
@@ -190,6 +208,15 @@ _SIGS = {
                                    C.POINTER(_P)]),
     "gck_set_profile": (C.c_int, [_P, C.c_uint32]),
     "gck_check_wait": (C.c_int, [_P, _P]),
+    "gck_check_bulk_at": (C.c_int, [_P, C.POINTER(_Consistency), _P, C.c_size_t, C.POINTER(C.c_char_p),
+                                    C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P, C.POINTER(C.c_uint64)]),
+    "gck_check_wait_at": (C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
+    "gck_check_bulk_uniform": (C.c_int, [_P, C.POINTER(_Consistency), C.POINTER(Uniform), _P, C.c_size_t,
+                                         C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P, _P,
+                                         C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]),
+    "gck_check_submit_uniform": (C.c_int, [_P, C.POINTER(_Consistency), C.POINTER(Uniform), _P, C.c_size_t,
+                                           C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_int64, _P,
+                                           _P, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(_P)]),
     "gck_host_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
     "gck_host_free": (C.c_int, [_P, _P]),
     "gck_last_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -281,6 +308,10 @@ def _driver():
         d.gckd_run_host.restype = C.c_int
         d.gckd_run_host.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_size_t, C.c_uint32, C.c_int64, C.POINTER(C.c_double)]
+        d.gckd_run_uniform.restype = C.c_int
+        d.gckd_run_uniform.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint32,
+                                       C.c_int64, C.POINTER(C.c_double)]
         d.gckd_set_trace.restype = None
         d.gckd_set_trace.argtypes = [C.c_void_p, C.c_size_t]
         _DRIVER = d
@@ -580,6 +611,80 @@ class Engine:
                                             perm.ctypes.data if n else None,
                                             err.ctypes.data if n else None))
         return perm, err
+
+    def check_bulk_at(self, items: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY,
+                      revision: int = 0, now_us: int = 0,
+                      contexts: Optional[Sequence] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+        """check_bulk plus the revision the batch was evaluated at (gck_check_bulk_at): the
+        response's CheckedAt."""
+        items = np.ascontiguousarray(items, dtype=ITEM_DTYPE)
+        n = len(items)
+        perm = np.zeros(n, dtype=np.uint8)
+        err = np.zeros(n, dtype=np.int32)
+        cs = _Consistency(requirement, 0, revision)
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        rev = C.c_uint64(0)
+        _check(self._lib.gck_check_bulk_at(self._h, C.byref(cs), items.ctypes.data if n else None, n, ctx_arr,
+                                           ctx_lens, n_ctx, now_us, perm.ctypes.data if n else None,
+                                           err.ctypes.data if n else None, C.byref(rev)))
+        return perm, err, rev.value
+
+    def check_uniform(self, header, pairs: np.ndarray, requirement: int = CONSISTENCY_MIN_LATENCY,
+                      revision: int = 0, now_us: int = 0, contexts: Optional[Sequence] = None,
+                      out_packed: Optional[np.ndarray] = None, out_errs: Optional[np.ndarray] = None):
+        """A uniform request (gck_check_bulk_uniform): `header` = (resource_type, permission,
+        subject_type, subject_relation, context_slot), `pairs` = (n, 2) u32 (resource id, subject
+        id). Returns (packed words, errors as ITEM_ERROR_DTYPE records, evaluated revision);
+        unpack_results(words, n) gives the Permissionships. Pinned output arrays (host_array) are
+        written in place by the kernels."""
+        pairs = np.ascontiguousarray(pairs, dtype=np.uint32).reshape(-1, 2)
+        n = len(pairs)
+        words = out_packed if out_packed is not None else np.zeros((n + 31) // 32, dtype=np.uint64)
+        errs = out_errs if out_errs is not None else np.zeros(n, dtype=ITEM_ERROR_DTYPE)
+        cs = _Consistency(requirement, 0, revision)
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        hdr = Uniform(*header[:4], header[4] if len(header) > 4 else 0, 0)
+        n_errs = C.c_size_t(0)
+        rev = C.c_uint64(0)
+        _check(self._lib.gck_check_bulk_uniform(self._h, C.byref(cs), C.byref(hdr), pairs.ctypes.data if n else None,
+                                                n, ctx_arr, ctx_lens, n_ctx, now_us,
+                                                words.ctypes.data if n else None, errs.ctypes.data if len(errs) else None,
+                                                len(errs), C.byref(n_errs), C.byref(rev)))
+        return words, errs[:min(n_errs.value, len(errs))].copy(), rev.value
+
+    def submit_uniform(self, header, pairs: np.ndarray, out_packed: np.ndarray, out_errs: np.ndarray,
+                       requirement: int = CONSISTENCY_MIN_LATENCY, revision: int = 0, now_us: int = 0,
+                       contexts: Optional[Sequence] = None) -> "UniformBatch":
+        """gck_check_submit_uniform: the results land in out_packed / out_errs at wait()."""
+        n = len(pairs)
+        cs = _Consistency(requirement, 0, revision)
+        ctx_arr, ctx_lens, n_ctx = _context_arrays(contexts)
+        hdr = Uniform(*header[:4], header[4] if len(header) > 4 else 0, 0)
+        b = UniformBatch(self, hdr, pairs, out_packed, out_errs)
+        _check(self._lib.gck_check_submit_uniform(self._h, C.byref(cs), C.byref(hdr), pairs.ctypes.data if n else None,
+                                                  n, ctx_arr, ctx_lens, n_ctx, now_us,
+                                                  out_packed.ctypes.data if n else None,
+                                                  out_errs.ctypes.data if len(out_errs) else None, len(out_errs),
+                                                  C.byref(b._n_errs), C.byref(b._h)))
+        return b
+
+    def run_uniform_batches(self, header, pairs, packed, errs, err_cap: int, n: int, depth: int,
+                            now_us: int = 0) -> float:
+        """The compiled submit/wait loop over uniform requests (libgck_driver.so gckd_run_uniform):
+        host pointers pairs[k], packed[k], errs[k], n checks each, `depth` in flight. Returns the
+        loop's wall time in seconds."""
+        drv = _driver()
+        k = len(pairs)
+        arr = lambda xs: (C.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
+        cs = _Consistency(CONSISTENCY_MIN_LATENCY, 0, 0)
+        hdr = Uniform(*header[:4], header[4] if len(header) > 4 else 0, 0)
+        n_errs = (C.c_size_t * max(1, k))()
+        secs = C.c_double(0.0)
+        submit = C.cast(self._lib.gck_check_submit_uniform, C.c_void_p)
+        wait = C.cast(self._lib.gck_check_wait, C.c_void_p)
+        _check(drv.gckd_run_uniform(submit, wait, self._h, C.byref(cs), C.byref(hdr), k, arr(pairs), arr(packed),
+                                    arr(errs), err_cap, n_errs, n, depth, now_us, C.byref(secs)))
+        return secs.value
 
     def check_bulk_device(self, d_items: int, n: int, d_perm: int, d_err: int,
                           stream: Optional[int] = None, now_us: int = 0,
@@ -890,12 +995,42 @@ class Batch:
         self._engine, self._h = engine, handle
         self.perm, self.err = perm, err
         self._items = items  # host items stay alive until the wait (they are staged at submit anyway)
+        self.revision = None  # the revision the batch ran on (gck_check_wait_at), after wait()
 
     def wait(self):
         if self._h is not None:
             h, self._h = self._h, None
-            _check(self._engine._lib.gck_check_wait(self._engine._h, h))
+            rev = C.c_uint64(0)
+            _check(self._engine._lib.gck_check_wait_at(self._engine._h, h, C.byref(rev)))
+            self.revision = rev.value
         return self.perm, self.err
+
+    def __del__(self):
+        try:
+            self.wait()
+        except Exception:
+            pass
+
+
+class UniformBatch:
+    """A submitted uniform request (gck_check_submit_uniform): wait() completes it exactly once and
+    returns (packed words, errors, evaluated revision)."""
+
+    def __init__(self, engine, hdr, pairs, packed, errs):
+        self._engine, self._hdr, self._pairs = engine, hdr, pairs
+        self.packed, self.errs = packed, errs
+        self._h = _P()
+        self._n_errs = C.c_size_t(0)
+        self.revision = None
+
+    def wait(self):
+        if self._h is not None and self._h.value is not None:
+            h, self._h = self._h, None
+            rev = C.c_uint64(0)
+            _check(self._engine._lib.gck_check_wait_at(self._engine._h, h, C.byref(rev)))
+            self.revision = rev.value
+        m = min(self._n_errs.value, len(self.errs))
+        return self.packed, self.errs[:m], self.revision
 
     def __del__(self):
         try:

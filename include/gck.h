@@ -36,6 +36,15 @@
  *   gck_set_head_revision
  *       the revision consistency.Full() (consistency/consistency.go:25-35) must reach: the
  *       ReadAt token of Client.ReadSchema (client/client.go:416-422) or a Watch checkpoint.
+ *   gck_check_bulk_at / gck_check_wait_at
+ *       the same calls, also returning the revision the batch was evaluated at: the response's
+ *       CheckedAt token (CheckBulkPermissionsResponse.CheckedAt, read by consistency users of
+ *       client/client.go:261-266).
+ *   gck_check_bulk_uniform / gck_check_submit_uniform
+ *       the common homogeneous request of Client.Check's item loop (client/client.go:241-259: one
+ *       CheckBulkPermissionsRequestItem per relationship, all of one resource type, permission,
+ *       subject type and subject relation) as one header and 8-byte (resource id, subject id)
+ *       pairs, answered as a packed 2-bit Permissionship plane plus a sparse per-item error list.
  *
  * Ownership: all inputs and outputs are caller-allocated; the engine never retains a caller
  * pointer after a call returns, except that gck_check_submit keeps the output pointers (and, for
@@ -58,7 +67,7 @@
 extern "C" {
 #endif
 
-#define GCK_ABI_VERSION 12
+#define GCK_ABI_VERSION 13
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define GCK_OK 0
@@ -374,6 +383,51 @@ int gck_reset_stats(gck_engine* e);
 /* Turns GCK_FLAG_PROFILE on or off for the batches submitted from now on (a timed batch brackets
  * its stage A with the kernel's own start/stop events, every 4th batch of a workspace). */
 int gck_set_profile(gck_engine* e, uint32_t on);
+
+/* The revision a check was evaluated at (ABI 13). gck_check_bulk_at is gck_check_bulk_ctx that
+ * also writes the revision of the snapshot the batch ran on to *out_revision (may be NULL): the
+ * response's CheckedAt. A submitted batch runs on the snapshot current at its submit, and
+ * gck_check_wait_at reports that revision — not the one current at the wait, which a Watch batch
+ * applied in between may have moved. */
+int gck_check_bulk_at(gck_engine* e, const gck_consistency* cs, const gck_item* items, size_t n,
+                      const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                      int64_t now_us, uint8_t* out_perm, int32_t* out_err, uint64_t* out_revision);
+int gck_check_wait_at(gck_engine* e, gck_batch* batch, uint64_t* out_revision);
+
+/* ---- uniform requests (ABI 13) -------------------------------------------------------
+ * A request whose items share (resource type, permission, subject type, subject relation, context
+ * slot) — what Client.Check sends for relationships of one shape (client/client.go:241-259) —
+ * travels as one header and n (resource id, subject id) pairs: 8 bytes per check over PCIe
+ * instead of 20. Results come back packed: check k's Permissionship (GCK_PERM_*) in bits
+ * 2(k mod 32) .. 2(k mod 32) + 1 of out_packed[k / 32] (ceil(n / 32) words; GCK_PERM_UNSPECIFIED
+ * for a check with an error), and the checks with an error as (index, GCK_ITEM_*) records in
+ * ascending index order: *out_n_errs = how many checks have one, the first min(that, err_cap) of
+ * them are written to out_errs. Semantics, consistency and request errors are gck_check_bulk_at's;
+ * a context_slot beyond n_contexts is GCK_E_INVALID_ARGUMENT. Pairs and results in gck_host_alloc
+ * memory are read and written in place by the kernels. */
+typedef struct gck_uniform {
+  uint16_t resource_type;
+  uint16_t permission;         /* global relation id (gck_relation_id) */
+  uint16_t subject_type;
+  uint16_t subject_relation;   /* GCK_ELLIPSIS for a concrete object */
+  uint32_t context_slot;       /* as gck_item.context_slot, for every pair */
+  uint32_t reserved;           /* 0 */
+} gck_uniform;                 /* 16 bytes */
+typedef struct gck_item_error {
+  uint32_t index;              /* the check's position in the request */
+  int32_t code;                /* GCK_ITEM_* (never GCK_ITEM_OK) */
+} gck_item_error;
+int gck_check_bulk_uniform(gck_engine* e, const gck_consistency* cs, const gck_uniform* hdr, const uint32_t* pairs,
+                           size_t n, const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                           int64_t now_us, uint64_t* out_packed, gck_item_error* out_errs, size_t err_cap,
+                           size_t* out_n_errs, uint64_t* out_revision);
+/* The same as an asynchronous batch (n <= max_batch; host buffers): completed by gck_check_wait or
+ * gck_check_wait_at, which write out_packed, out_errs and *out_n_errs. `pairs`, `hdr` and the
+ * outputs must stay valid until the wait returns. */
+int gck_check_submit_uniform(gck_engine* e, const gck_consistency* cs, const gck_uniform* hdr, const uint32_t* pairs,
+                             size_t n, const char* const* contexts, const size_t* context_lens, size_t n_contexts,
+                             int64_t now_us, uint64_t* out_packed, gck_item_error* out_errs, size_t err_cap,
+                             size_t* out_n_errs, gck_batch** out);
 
 /* ---- lookups (Client.LookupResources / LookupSubjects, client/client.go:508-599) -------- */
 /* Ids of the `resource_type` objects on which the subject has `permission` — HAS or CONDITIONAL,

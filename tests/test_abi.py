@@ -37,6 +37,7 @@ def test_driver_library_exports_its_loop():
     import os
     path = os.path.join(os.path.dirname(E.__file__), "libgck_driver.so")
     assert hasattr(ctypes.CDLL(path), "gckd_run")
+    assert hasattr(ctypes.CDLL(path), "gckd_run_uniform")
 
 
 def test_struct_layouts_match_header():
@@ -45,7 +46,9 @@ def test_struct_layouts_match_header():
     assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
     assert C.sizeof(E._Stats) == 232
-    assert E.load_library().gck_abi_version() == 12
+    assert C.sizeof(E.Uniform) == 16
+    assert E.ITEM_ERROR_DTYPE.itemsize == 8
+    assert E.load_library().gck_abi_version() == 13
 
 
 @pytest.fixture()
@@ -150,6 +153,31 @@ def test_state_errors(eng):
     with pytest.raises(E.GckError) as ei:
         eng.apply_updates(2, np.zeros(1, dtype=E.UPDATE_DTYPE))
     assert ei.value.code == E.GCK_E_STATE
+
+
+def test_uniform_and_revision_entry_points_without_a_snapshot(eng):
+    """The ABI-13 entry points validate their arguments on the host: a uniform header whose context
+    slot exceeds the contexts given is refused before anything else, an empty request needs a
+    snapshot like any check, and a submitted batch's revision is the one at submit."""
+    with pytest.raises(E.GckError) as ei:
+        eng.check_uniform((0, 0, 0, 0xFFFF, 2), np.zeros((4, 2), dtype=np.uint32), contexts=[{"a": 1}])
+    assert ei.value.code == E.GCK_E_INVALID_ARGUMENT
+    eng.load_schema("definition user {}")
+    with pytest.raises(E.GckError) as ei:
+        eng.check_uniform((0, 0, 0, 0xFFFF), np.zeros((0, 2), dtype=np.uint32))
+    assert ei.value.code == E.GCK_E_STATE
+    with pytest.raises(E.GckError) as ei:
+        eng.check_bulk_at(np.zeros(0, dtype=E.ITEM_DTYPE))
+    assert ei.value.code == E.GCK_E_STATE
+
+
+def test_unpack_results_layout():
+    """Packed results: check k in bits 2(k mod 32) of little-endian word k / 32."""
+    perm = np.array([1, 2, 3, 0] * 20 + [2], dtype=np.uint8)
+    words = np.zeros((len(perm) + 31) // 32, dtype=np.uint64)
+    for k, p in enumerate(perm):
+        words[k // 32] |= np.uint64(int(p) << (2 * (k % 32)))
+    assert E.unpack_results(words, len(perm)).tolist() == perm.tolist()
 
 
 def test_watch_staging_without_a_snapshot():
