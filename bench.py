@@ -99,9 +99,10 @@ def parse():
                          "tuples, check contexts, one Watch batch of --churn x tuples applied per step); quota = "
                          "config 5 with 32K per-relationship caveat contexts x one context per request")
     ap.add_argument("--selftest", action="store_true", help="launcher / rank bookkeeping only (no GPU; tests)")
-    ap.add_argument("--coalesce", type=int, default=None,
+    ap.add_argument("--coalesce", type=int, default=1,
                     help="strong scaling: a rank checks its slices of up to this many consecutive requests in one "
-                         "dispatch (default: the ranks, so a dispatch is again ~--batch checks; 1 = one per request)")
+                         "dispatch (default 1: one dispatch per request slice, so `value` at N > 1 is strong scaling "
+                         "of one 64K request; with N > 1 the figure at coalesce = N is reported as `coalesced`)")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--watch-stage", type=int, default=1,
                     help="config 5: stage the next step's Watch batch (gck_watch_stage: grouped on the engine's "
@@ -329,6 +330,53 @@ def selftest(args):
         dist.destroy_process_group()
 
 
+def roofline_line(tj, tj_path, b_alg, ms, steps, job_s):
+    """The roofline object of the dominant kernel. `achieved` = the HBM bytes one launch moves —
+    rocprofv3 FETCH_SIZE + WRITE_SIZE of this workload's batches on this round's code (`tj`,
+    tools/traffic_summary.py) — over the mean solo launch time `ms`; `frac` = that / 8 TB/s, and
+    `frac_job` the same bytes of every timed batch over the device-resident timed region `job_s`.
+    SURVEY §8(d)'s algorithmic bytes (`alg_bytes_per_launch`) charge the forward search the joins
+    replace with precomputed slots, so their ratio to the time is no HBM fraction and is not
+    reported as one. The joins are random-line bound: `random_lines` compares the 64-B accesses per
+    launch (FETCH_SIZE / 64: every random read of <= 64 B counts one line, tools/gather_probe) with
+    the random-line rate tools/gather_probe measured in the same profile run."""
+    root = os.path.dirname(os.path.abspath(__file__))
+    traffic = tj.get("hbm_bytes_per_batch") if tj else None
+    src = os.path.relpath(tj_path, root) if tj else None
+    sec = ms * 1e-3
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic, "traffic_source": src,
+            "alg_bytes_per_launch": int(b_alg),
+            "alg_note": "SURVEY §8(d) algorithmic bytes (25 B per check + 8 B per row + 4 B per edge of the oracle's "
+                        "forward BFS): the joins answer from precomputed slots and never perform that BFS, so these "
+                        "bytes over the launch time are not an HBM fraction (they exceed the peak at job level); "
+                        "achieved / frac use the measured bytes"}
+    if traffic:
+        roof["achieved"] = round(traffic / sec / 1e9, 3)
+        roof["frac"] = round(traffic / sec / 1e9 / HBM_PEAK_GBS, 6)
+        if job_s:
+            roof["achieved_job"] = round(traffic * steps / job_s / 1e9, 3)
+            roof["frac_job"] = round(traffic * steps / job_s / 1e9 / HBM_PEAK_GBS, 6)
+        fetch = sum((tj.get("fetch_bytes_raw_per_launch") or {}).get(k, 0) for k in tj.get("kernels", []))
+        ceil = (tj.get("line_ceiling") or {}).get("64")
+        if fetch:
+            lines = fetch / 64.0
+            rl = {"per_launch": int(lines), "solo_G_per_s": round(lines / sec / 1e9, 2)}
+            if job_s:
+                rl["job_G_per_s"] = round(lines * steps / job_s / 1e9, 2)
+            if ceil:
+                rl["ceiling_G_per_s"] = ceil
+                rl["frac_solo"] = round(rl["solo_G_per_s"] / ceil, 4)
+                if job_s:
+                    rl["frac_job"] = round(rl["job_G_per_s"] / ceil, 4)
+                rl["ceiling_source"] = "tools/gather_probe: random aligned 64-B reads from a table 16x the Infinity Cache"
+            roof["random_lines"] = rl
+    else:  # no counter pass for this workload on this round's code: the algorithmic figure, flagged
+        roof["achieved"] = round(b_alg / sec / 1e9, 3)
+        roof["frac"] = round(b_alg / sec / 1e9 / HBM_PEAK_GBS, 6)
+        roof["achieved_basis"] = "algorithmic bytes (no PMC pass found for this workload)"
+    return roof
+
+
 def progress(msg):
     """Progress on stderr (long runs under a profiler must keep writing)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -525,8 +573,9 @@ def main():
         # its slices of up to `coal` consecutive requests in one dispatch (they are contiguous), as a
         # node-level dispatcher batches what arrives for each GPU. The timed region still holds
         # exactly the steps' requests. coal_for(count): the largest divisor of count <= coal.
-        coal = max(1, min(args.coalesce if args.coalesce else world, max(1, args.batch // max(1, n_slice))))
-        coal_for = lambda count: max(c for c in range(1, coal + 1) if count % c == 0)
+        coal_max = max(1, args.batch // max(1, n_slice))
+        coal = max(1, min(args.coalesce, coal_max))
+        coal_for = lambda count, cap=None: max(c for c in range(1, (cap or coal) + 1) if count % c == 0)
         streams = [torch.cuda.Stream(dev) for _ in range(depth)]
         # `value`'s path (BASELINE.md:40-41, SURVEY §8d: items H2D + kernels + results D2H): the
         # same requests in host memory — pinned, from gck_host_alloc, where a cgo caller builds its
@@ -623,8 +672,8 @@ def main():
     # of their own, on the engine's streams.
     device_resident = None
     if pipelined:
-        def mkd(k0, count):
-            cc = coal_for(count)
+        def mkd(k0, count, cap=None):
+            cc = coal_for(count, cap)
             ks = range(k0, k0 + count, cc)
             return eng.prepare_batches([rot[k].data_ptr() for k in ks], [outs[k][0].data_ptr() for k in ks],
                                        [outs[k][1].data_ptr() for k in ks], n_slice * cc, depth,
@@ -653,6 +702,32 @@ def main():
                            "note": "the same rotated requests with the items already in HBM and the results left "
                                    "there (no PCIe in the step): `value`"}
         progress(f"device-resident phase: {td * 1e3:.2f} ms")
+    # N > 1: the same device-resident requests with a rank's slices of N consecutive requests in one
+    # dispatch (what a node-level dispatcher that aggregates per GPU would do): N x the per-request
+    # latency, so reported beside `value`, never as it
+    coalesced = None
+    if pipelined and world > 1 and args.coalesce == 1 and coal_max > 1:
+        c_warm, c_run = mkd(0, args.warm, coal_max), mkd(args.warm, args.steps, coal_max)
+        torch.cuda.synchronize()
+        c_warm.run()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        c_run.run()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tc = time.perf_counter() - tc
+        tt = torch.tensor([tc], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tc = float(tt[0])
+        coalesced = {"value": round(args.batch * args.steps / tc, 1), "unit": "checks/s",
+                     "requests_per_dispatch": coal_for(args.steps, coal_max),
+                     "checks_per_dispatch": n_slice * coal_for(args.steps, coal_max),
+                     "ms_per_step": round(tc / args.steps * 1e3, 4),
+                     "note": "device-resident, a rank's slices of consecutive requests checked in one dispatch "
+                             "(request aggregation: each request waits for the next ones); not `value`"}
+        progress(f"coalesced phase: {tc * 1e3:.2f} ms")
     # weak scaling beside the node figure (N > 1): every rank checks its own whole requests (host
     # buffers, as `value`)
     weak = None
@@ -833,6 +908,109 @@ def main():
                              "buffers (`python_pinned`), pageable numpy buffers through the engine's pinned staging "
                              "(`pageable`), 1 in flight (`one_at_a_time`)"}
 
+    # ---- the uniform caller format (include/gck.h gck_check_submit_uniform; never `value`): the same
+    # requests as runs of one shape — one header, 8-B (resource id, subject id) pairs in pinned host
+    # memory, packed 2-bit results and a sparse error list back, read and written in place by the
+    # join — `depth` in flight through the compiled loop. Each request is cut into its shapes
+    # (config 4: one; configs 2 / 3: a run per permission), as INTEGRATION.md's toItems does.
+    uni_line = None
+    if pipelined and args.host_steps > 0:
+        from gochugaru_amd.engine import ITEM_ERROR_DTYPE, unpack_results
+        from gochugaru_amd.engine import _driver
+        import ctypes
+        n_u = args.warm + args.steps
+        u_pairs = eng.host_array(n_u * n_slice * 2, np.uint32)
+        u_errs = eng.host_array(n_u * n_slice, ITEM_ERROR_DTYPE)
+        groups = []  # per uniform request: (batch k, header, start offset in the batch, order slice)
+        words = 0
+        for k in range(n_u):
+            hk = h_items[k * n_slice:(k + 1) * n_slice]
+            key = ((hk["resource_type"].astype(np.uint64) << np.uint64(48)) | (hk["permission"].astype(np.uint64) << np.uint64(32))
+                   | (hk["subject_type"].astype(np.uint64) << np.uint64(16)) | hk["subject_relation"].astype(np.uint64))
+            order = np.argsort(key, kind="stable")
+            pv = u_pairs[2 * k * n_slice:2 * (k + 1) * n_slice].reshape(-1, 2)
+            pv[:, 0] = hk["resource_id"][order]
+            pv[:, 1] = hk["subject_id"][order]
+            ks = key[order]
+            cuts = [0] + (np.flatnonzero(np.diff(ks)) + 1).tolist() + [n_slice]
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                x = int(ks[a])
+                hdr = ((x >> 48) & 0xFFFF, (x >> 32) & 0xFFFF, (x >> 16) & 0xFFFF, x & 0xFFFF, 0)
+                groups.append((k, hdr, a, b, order[a:b], words))
+                words += (b - a + 31) // 32
+        u_packed = eng.host_array(max(1, words), np.uint64)
+        g_warm = [g for g in groups if g[0] < args.warm]
+        g_time = [g for g in groups if g[0] >= args.warm]
+
+        def prep_u(gs, dq):
+            return eng.prepare_uniform([g[1] for g in gs],
+                                       [u_pairs.ctypes.data + 8 * (g[0] * n_slice + g[2]) for g in gs],
+                                       [g[3] - g[2] for g in gs],
+                                       [u_packed.ctypes.data + 8 * g[5] for g in gs],
+                                       [u_errs.ctypes.data + 8 * (g[0] * n_slice + g[2]) for g in gs],
+                                       n_slice, dq)
+        pw, pt = prep_u(g_warm, depth), prep_u(g_time, depth)
+        pw.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tu = time.perf_counter()
+        pt.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tu = time.perf_counter() - tu
+        if world > 1:
+            tt = torch.tensor([tu], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tu = float(tt[0])
+        # every timed request's results against the item path's (the timed region above)
+        same_u = True
+        for gi, (k, hdr, a, b, order_g, w0) in enumerate(g_time):
+            n_g = b - a
+            got = unpack_results(u_packed[w0:w0 + (n_g + 31) // 32], n_g)
+            ne = int(pt.n_errs[gi])
+            rec = u_errs[k * n_slice + a:k * n_slice + a + min(ne, n_g)]
+            e_g = np.zeros(n_g, dtype=np.int32)
+            e_g[rec["index"]] = rec["code"]
+            hp = h_perm[k * n_slice:(k + 1) * n_slice][order_g]
+            he = h_err[k * n_slice:(k + 1) * n_slice][order_g]
+            want_p = np.where(he != 0, 0, hp)
+            if not ((got == want_p).all() and (e_g == he).all()):
+                same_u = False
+                break
+        # one request at a time (BASELINE.md:40-41's lone-batch step in the uniform format): the
+        # first rotated requests, 1 in flight, median over >= 20 after 3 warm-up ones
+        g_lone = [g for g in groups if g[0] < min(n_u, 23)]
+        pl = prep_u(g_lone, 1)
+        stamps = np.zeros(2 * len(g_lone), dtype=np.float64)
+        _driver().gckd_set_trace(stamps.ctypes.data_as(ctypes.c_void_p), len(g_lone))
+        pl.run()
+        _driver().gckd_set_trace(None, 0)
+        ends = stamps[1::2]
+        starts = np.concatenate([[0.0], ends[:-1]])
+        per_req = (ends - starts)
+        per_batch = collections.defaultdict(float)
+        for g, t in zip(g_lone, per_req):
+            per_batch[g[0]] += t
+        lone = [per_batch[k] for k in sorted(per_batch)][3:]
+        med_u = float(np.median(lone)) if lone else None
+        per_rank = args.batch * args.steps / world
+        uni_line = {"value": round(args.batch * args.steps / tu, 1), "unit": "checks/s",
+                    "ms_per_step": round(tu / args.steps * 1e3, 4), "inflight": depth,
+                    "requests_per_batch": round(len(g_time) / args.steps, 2),
+                    "same_results_as_items": bool(same_u),
+                    "bytes_per_check": {"h2d": 8, "d2h": 0.25},
+                    "pcie_h2d_GBs": round(per_rank * 8 / tu / 1e9, 2),
+                    "lone_batch": ({"value": round(n_slice / med_u, 1), "median_batch_ms": round(med_u * 1e3, 4),
+                                    "batches": len(lone)} if med_u else None),
+                    "definition": "the timed requests as uniform requests (gck_check_submit_uniform: one header + "
+                                  "8-B id pairs in pinned host memory, 2-bit results + error list back, read and "
+                                  "written in place by the join across PCIe), 8 in flight through the compiled loop "
+                                  "(gckd_run_uniform); `lone_batch`: one 64K request at a time, median"}
+        del u_pairs, u_errs, u_packed
+        progress(f"uniform phase: {tu * 1e3:.2f} ms")
+
     # `value`'s path is bound by the host link: 20 B of items in and 5 B of results out per check
     pcie = None
     if WL.kind in ("nested", "gdocs", "github") and not args.partitioned:
@@ -919,44 +1097,29 @@ def main():
         ms_a = st_roof["bundle_ms"] / st_roof["bundle_launches"]
         ms_b = st_roof["giant_ms"] / st_roof["bundle_launches"]
         ms = ms_a + ms_b
-        achieved = b_alg / (ms * 1e-3) / 1e9
-        traffic, traffic_src = None, None
-        # (the counter passes of this workload's own batches, tools/gpu.sh profile)
+        tj = None
+        # (the counter passes of this workload's own batches on this round's code: tools/gpu.sh profile)
         if args.traffic_json is None:
-            args.traffic_json = os.path.join(ROOT, "profiles", "r04", {"nested": "aql_pmc", "gdocs": "pmc_gdocs",
-                                                                        "github": "pmc_github"}.get(WL.kind, "-"),
-                                             "traffic.json")
+            args.traffic_json = os.path.join(ROOT, "profiles", "r06", "pmc_" + WL.kind, "traffic.json")
         if args.traffic_json and os.path.exists(args.traffic_json) and WL.kind in ("nested", "gdocs", "github"):
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("hbm_bytes_per_batch")
-            traffic_src = os.path.relpath(args.traffic_json, os.path.dirname(os.path.abspath(__file__)))
+        roof = roofline_line(tj, args.traffic_json, b_alg, ms, args.steps,
+                             device_resident["seconds"] if device_resident else None)
         # the join stage A ran: the label join (labels.inc) when the snapshot has label tables
         # and prefers them, else the closure join (closure.inc)
         kname = "k_label_join" if st_roof.get("label_checks", 0) > 0 else "k_closure_join"
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                "kernel": (f"{kname} (+ k_bundles<1> over what it leaves): stage A of a batch, dispatched as in "
-                           "the timed region (into the engine's HSA queues, aql.inc) and timed by the queue's dispatch "
-                           "timestamps (hsa_amd_profiling_get_dispatch_time: packet start to completion), batches one "
-                           "at a time after the timed region; k_bundles<16> only for deferred giant checks"),
-                "alg_bytes_per_launch": int(b_alg),
-                # the whole job: algorithmic bytes of every timed batch / the timed region (launches
-                # of consecutive batches overlap when --inflight > 1, so this exceeds `achieved`)
-                "achieved_job": round(b_alg * args.steps / device_resident["seconds"] / 1e9, 3)
-                if device_resident else None,
-                "inflight": depth,
-                "driver": args.driver if run_steps is not None or args.driver == "python" else "python",
-                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or 4,
-                "engine_streams": bool(args.engine_streams),
-                "launch_timing": "solo" if st_solo is not None else "timed region",
-                "alg_counts": {k: int(v) for k, v in cnt.items()},
-                "mean_launch_ms": {f"stage A ({kname} + k_bundles<1>)": round(ms_a, 4),
-                                   "k_bundles<16>": round(ms_b, 4)},
-                "traffic_source": traffic_src,
-                "note": "latency-bound: a check is two dependent rounds of random 64-B lines (items, then its "
-                        "user and resource slots; label / closure join); the algorithmic bytes charge the forward BFS "
-                        "the engine avoids, so `traffic` (the lines actually moved) is below them; the batches "
-                        "in flight overlap, hence achieved_job > achieved; see DESIGN.md"}
+        roof.update({
+            "kernel": (f"{kname} (+ k_bundles<1> over what it leaves): stage A of a batch, dispatched as in "
+                       "the timed region (into the engine's HSA queues, aql.inc) and timed by the queue's dispatch "
+                       "timestamps (hsa_amd_profiling_get_dispatch_time: packet start to completion), batches one "
+                       "at a time after the timed region; k_bundles<16> only for deferred giant checks"),
+            "inflight": depth,
+            "driver": args.driver if run_steps is not None or args.driver == "python" else "python",
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or 4,
+            "engine_streams": bool(args.engine_streams),
+            "launch_timing": "solo" if st_solo is not None else "timed region",
+            "alg_counts": {k: int(v) for k, v in cnt.items()},
+            "mean_launch_ms": {f"stage A ({kname} + k_bundles<1>)": round(ms_a, 4), "k_bundles<16>": round(ms_b, 4)}})
 
     # ---- CPU baseline: the C restatement oracle on a bounded sample (rank 0, N=1) -----------
     # The sample is the timed batch plus further batches of the same generator (other seeds),
@@ -1025,21 +1188,15 @@ def main():
         # events every 4th batch of a workspace inside the timed region; the Watch batch is
         # the rest of the step (watch.apply_ms_per_step)
         ms_a = (st["bundle_ms"] + st["giant_ms"]) / st["bundle_launches"]
-        achieved = mixed_alg / (ms_a * 1e-3) / 1e9
         # (the counter passes of config 5's own check batches, tools/gpu.sh profile ... --config mixed)
-        tj_path = args.traffic_json or os.path.join(ROOT, "profiles", "r05", "pmc_mixed", "traffic.json")
-        m_traffic, m_src = None, None
-        if os.path.exists(tj_path):
-            m_traffic = json.load(open(tj_path)).get("hbm_bytes_per_batch")
-            m_src = os.path.relpath(tj_path, os.path.dirname(os.path.abspath(__file__)))
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": m_traffic, "traffic_source": m_src,
-                "kernel": ("stage A of the check batch: k_label_join with the caveat plane, then k_bundles<1> over "
-                           "the checks it deferred" if st["label_checks"] > 0 else
-                           "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks)")
-                          + ", HIP events on its launch stream, sampled every 4th batch in the timed region",
-                "alg_bytes_per_launch": int(mixed_alg), "mean_launch_ms": round(ms_a, 4),
-                "achieved_job": round(mixed_alg * args.steps / elapsed / 1e9, 3)}
+        tj_path = args.traffic_json or os.path.join(ROOT, "profiles", "r06", "pmc_mixed", "traffic.json")
+        tj = json.load(open(tj_path)) if os.path.exists(tj_path) else None
+        roof = roofline_line(tj, tj_path, mixed_alg, ms_a, args.steps, elapsed)
+        roof.update({"kernel": ("stage A of the check batch: k_label_join with the caveat plane, then k_bundles<1> over "
+                                "the checks it deferred" if st["label_checks"] > 0 else
+                                "stage A of the check batch (k_bundles<1>; k_bundles<16> for deferred giant checks)")
+                               + ", HIP events on its launch stream, sampled every 4th batch in the timed region",
+                     "mean_launch_ms": round(ms_a, 4)})
 
     if rank == 0 and args.partitioned and prog is not None:  # rank 0's slice of the global batch
         t_c = time.perf_counter()
@@ -1127,8 +1284,11 @@ def main():
                                                                   "none was found, so the C restatement stands in")}}
                              if cpu else cpu),
             **({"dispatch": {"requests_per_dispatch": coal_for(args.steps), "checks_per_dispatch": n_slice * coal_for(args.steps),
-                             "note": "a rank's slices of consecutive requests checked in one dispatch (--coalesce)"}}
+                             "note": "a rank's slices of consecutive requests checked in one dispatch (--coalesce; "
+                                     "1 = strong scaling of each request)"}}
                if strong and world > 1 else {}),
+            **({"coalesced": coalesced} if coalesced else {}),
+            **({"baseline_pipelined_uniform": uni_line} if uni_line else {}),
             **({"baseline_pipelined": baseline_pipelined} if baseline_pipelined else {}),
             **({"baseline_step": baseline_step} if baseline_step else {}),
             **({"weak_scaling": weak} if weak else {}),

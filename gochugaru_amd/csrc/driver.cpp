@@ -104,12 +104,13 @@ int gckd_run_host(submit_fn submit, wait_fn wait, gck_engine* e, const gck_consi
   return rc;
 }
 
-// The same loop over uniform requests (gck_check_submit_uniform): one header, host pairs[k] (n pairs
-// of u32 ids) in, packed[k] (ceil(n / 32) words) and errs[k] (err_cap records, the count in
-// n_errs[k]) out — what Client.Check sends for relationships of one shape, in 8 B per check.
-int gckd_run_uniform(submit_uniform_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs,
-                     const gck_uniform* hdr, size_t n_batches, const uint64_t* pairs, const uint64_t* packed,
-                     const uint64_t* errs, size_t err_cap, size_t* n_errs, size_t n, uint32_t depth, int64_t now_us,
+// The same loop over uniform requests (gck_check_submit_uniform): request k = header hdrs[k] and
+// ns[k] host pairs pairs[k] (u32 ids) in, packed[k] (ceil(ns[k] / 32) words) and errs[k] (err_cap
+// records, the count in n_errs[k]) out — what Client.Check sends for runs of relationships of one
+// shape, 8 B per check.
+int gckd_run_uniform(submit_uniform_fn submit, wait_fn wait, gck_engine* e, const gck_consistency* cs, size_t n_batches,
+                     const gck_uniform* hdrs, const uint64_t* pairs, const uint64_t* ns, const uint64_t* packed,
+                     const uint64_t* errs, size_t err_cap, size_t* n_errs, uint32_t depth, int64_t now_us,
                      double* seconds) {
   if (depth == 0) depth = 1;
   std::deque<gck_batch*> q;
@@ -123,8 +124,8 @@ int gckd_run_uniform(submit_uniform_fn submit, wait_fn wait, gck_engine* e, cons
       if (rc != GCK_OK) break;
     }
     gck_batch* b = nullptr;
-    rc = submit(e, cs, hdr, reinterpret_cast<const uint32_t*>(pairs[k]), n, nullptr, nullptr, 0, now_us,
-                reinterpret_cast<uint64_t*>(packed[k]), reinterpret_cast<gck_item_error*>(errs[k]), err_cap,
+    rc = submit(e, cs, hdrs + k, reinterpret_cast<const uint32_t*>(pairs[k]), (size_t)ns[k], nullptr, nullptr, 0,
+                now_us, reinterpret_cast<uint64_t*>(packed[k]), reinterpret_cast<gck_item_error*>(errs[k]), err_cap,
                 n_errs ? n_errs + k : nullptr, &b);
     if (rc == GCK_OK) q.push_back(b);
     stamp(t0, k, 0);

@@ -309,8 +309,8 @@ def _driver():
         d.gckd_run_host.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_size_t, C.c_uint32, C.c_int64, C.POINTER(C.c_double)]
         d.gckd_run_uniform.restype = C.c_int
-        d.gckd_run_uniform.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
-                                       C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint32,
+        d.gckd_run_uniform.argtypes = [C.c_void_p, C.c_void_p, _P, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
                                        C.c_int64, C.POINTER(C.c_double)]
         d.gckd_set_trace.restype = None
         d.gckd_set_trace.argtypes = [C.c_void_p, C.c_size_t]
@@ -668,23 +668,19 @@ class Engine:
                                                   C.byref(b._n_errs), C.byref(b._h)))
         return b
 
+    def prepare_uniform(self, headers, pairs, ns, packed, errs, err_cap: int, depth: int,
+                        now_us: int = 0) -> "PreparedUniform":
+        """The compiled submit/wait loop over uniform requests (libgck_driver.so gckd_run_uniform),
+        its arguments marshalled ahead: request k = headers[k] (gck_uniform fields) and host pointers
+        pairs[k] (ns[k] pairs), packed[k], errs[k] (err_cap records), `depth` in flight."""
+        return PreparedUniform(self, headers, pairs, ns, packed, errs, err_cap, depth, now_us)
+
     def run_uniform_batches(self, header, pairs, packed, errs, err_cap: int, n: int, depth: int,
                             now_us: int = 0) -> float:
-        """The compiled submit/wait loop over uniform requests (libgck_driver.so gckd_run_uniform):
-        host pointers pairs[k], packed[k], errs[k], n checks each, `depth` in flight. Returns the
-        loop's wall time in seconds."""
-        drv = _driver()
+        """prepare_uniform(...).run() for requests of one header and n checks each; returns the loop's
+        wall time in seconds."""
         k = len(pairs)
-        arr = lambda xs: (C.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
-        cs = _Consistency(CONSISTENCY_MIN_LATENCY, 0, 0)
-        hdr = Uniform(*header[:4], header[4] if len(header) > 4 else 0, 0)
-        n_errs = (C.c_size_t * max(1, k))()
-        secs = C.c_double(0.0)
-        submit = C.cast(self._lib.gck_check_submit_uniform, C.c_void_p)
-        wait = C.cast(self._lib.gck_check_wait, C.c_void_p)
-        _check(drv.gckd_run_uniform(submit, wait, self._h, C.byref(cs), C.byref(hdr), k, arr(pairs), arr(packed),
-                                    arr(errs), err_cap, n_errs, n, depth, now_us, C.byref(secs)))
-        return secs.value
+        return self.prepare_uniform([header] * k, pairs, [n] * k, packed, errs, err_cap, depth, now_us).run()
 
     def check_bulk_device(self, d_items: int, n: int, d_perm: int, d_err: int,
                           stream: Optional[int] = None, now_us: int = 0,
@@ -985,6 +981,31 @@ class PreparedRun:
             _check(self._drv.gckd_run(self._submit, self._wait, self._e._h, C.byref(self._cs), self._k, self._items,
                                       self._perms, self._errs, self._n, self._depth, self._streams, self._flags,
                                       self._now, C.byref(self._secs)))
+        return self._secs.value
+
+
+class PreparedUniform:
+    """A compiled submit/wait loop over uniform requests with its argument arrays built
+    (Engine.prepare_uniform)."""
+
+    def __init__(self, engine, headers, pairs, ns, packed, errs, err_cap, depth, now_us):
+        arr = lambda xs: (C.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
+        self._e, self._k, self._depth, self._now, self._cap = engine, len(pairs), depth, now_us, err_cap
+        self._hdrs = (Uniform * max(1, len(headers)))(
+            *[Uniform(*h[:4], h[4] if len(h) > 4 else 0, 0) for h in headers])
+        self._pairs, self._ns, self._packed, self._errs = arr(pairs), arr(ns), arr(packed), arr(errs)
+        self.n_errs = (C.c_size_t * max(1, len(pairs)))()
+        self._cs = _Consistency(CONSISTENCY_MIN_LATENCY, 0, 0)
+        self._drv = _driver()
+        self._submit = C.cast(engine._lib.gck_check_submit_uniform, C.c_void_p)
+        self._wait = C.cast(engine._lib.gck_check_wait, C.c_void_p)
+        self._secs = C.c_double(0.0)
+
+    def run(self) -> float:
+        """Runs the loop; returns its wall time in seconds (first submit to last wait)."""
+        _check(self._drv.gckd_run_uniform(self._submit, self._wait, self._e._h, C.byref(self._cs), self._k,
+                                          self._hdrs, self._pairs, self._ns, self._packed, self._errs, self._cap,
+                                          self.n_errs, self._depth, self._now, C.byref(self._secs)))
         return self._secs.value
 
 

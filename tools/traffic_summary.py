@@ -68,7 +68,19 @@ def main(out):
     stage_a = [k for k in ("k_closure_join", "k_label_join", "k_bundles<1>") if k in fetch]
     factor = (calib.get(64) or {}).get("factor") or 1.0  # one 64-B line per random access
     raw = sum(fetch[k] for k in stage_a)
+    # the random-line ceiling of the same box: tools/gather_probe's random aligned reads per second
+    # (G accesses/s per width; median of its repeats) — the joins' bound (bench.py roofline_line)
+    rates = defaultdict(list)
+    for f in glob.glob(f"{out}/gather_plain.jsonl"):
+        for line in open(f):
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            rates[str(r["width"])].append(r["lanes"] / (r["ms"] * 1e-3) / 1e9)
+    ceiling = {w: round(sorted(v)[len(v) // 2], 2) for w, v in rates.items()}
     res = {
+        "line_ceiling": ceiling,
         "calibration": calib,
         "fetch_bytes_raw_per_launch": fetch, "write_bytes_per_launch": write, "launches": n_fetch,
         "fetch_factor_used": factor,
