@@ -1455,7 +1455,7 @@ int device_init(Engine& e) {
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-PhaseClock::PhaseClock(const char* w) : what(w), on(getenv("GCK_DEBUG_PHASES") != nullptr), t0(0), last(0) {
+PhaseClock::PhaseClock(const char* w) : what(w), on(debug_env("GCK_DEBUG_PHASES") != nullptr), t0(0), last(0) {
   if (on) t0 = last = now_s();
 }
 void PhaseClock::mark(const char* phase) {
@@ -1744,7 +1744,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
     // (a Watch batch does not wait here: what follows reads the merged arrays on the null stream
     // after the merge, or through a synchronous copy that waits for it; the publication waits for
     // the null stream before the snapshot is swapped in, device_apply_publish)
-    static const bool dbg_csr_sync = getenv("GCK_DEBUG_CSR_SYNC") != nullptr;
+    static const bool dbg_csr_sync = debug_env("GCK_DEBUG_CSR_SYNC") != nullptr;
     if (!delta) HIP_OK(hipDeviceSynchronize());
     else if (dbg_csr_sync) spin_stream(e, nullptr);
     pc.mark("csr_sync");
@@ -2361,7 +2361,7 @@ static BundleArgs bundle_args(Engine& e, Workspace& w, const gck_item* d_items, 
   a.fr_base = w.b_fr;
   a.vis_base = w.b_vis;
   a.vlog_base = w.b_vlog;
-  static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
+  static const bool dbg_on = debug_env("GCK_DEBUG_BUNDLE") != nullptr;
   if (dbg_on && !w.dbg) HIP_OK(hipMalloc(&w.dbg, (4 + kBQ * 6 + kBJ * 8) * 4));
   a.dbg = dbg_on ? w.dbg : nullptr;
   a.budget = w.b_budget;
@@ -2369,7 +2369,7 @@ static BundleArgs bundle_args(Engine& e, Workspace& w, const gck_item* d_items, 
   a.idx = nullptr;
   a.n_dev = nullptr;
   // GCK_DEBUG_TIMING=<file prefix>: per-bundle records (bundle.inc BundleArgs::timing) of both stages
-  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  static const char* timing_env = debug_env("GCK_DEBUG_TIMING");
   // bundle records of stages A and B, then the closure join's per-wave records
   const size_t timing_words = (size_t)kTimingWords * (n + 1) * 2 +
                               std::max((size_t)kCjTimingWords * (n / 64 + 1), (size_t)kLjTimingWords * (n / 16 + 1));
@@ -2491,7 +2491,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   Ctx c = make_ctx(e, w, now_us, st, false);  // (the bundles below wait for the index patch: wait_patch)
   c.ck_items = d_items;
   BundleArgs a = bundle_args(e, w, d_items, n, d_perm, d_err);
-  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  static const char* timing_env = debug_env("GCK_DEBUG_TIMING");
   if (timing_env) HIP_OK(hipMemsetAsync(w.timing, 0, w.timing_cap * 8, st));
   const bool ctr_was_clean = w.ctr_clean && !timing_env;
   if (!w.ctr_clean) HIP_OK(hipMemsetAsync(w.ctr, 0, sizeof(DevCounters) + kBCtrs * sizeof(unsigned), st));  // + b_ctrs
@@ -2539,7 +2539,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // (GCK_DEBUG_HIP_SELFPUB: an engine-stream batch launched through HIP publishes itself from its
   // last block as an AQL-dispatched one does — the dispatch-span attribution of tools/aql_span.sh;
   // its results are not written back before the publication, so only device readers may use them)
-  static const bool dbg_selfpub = getenv("GCK_DEBUG_HIP_SELFPUB") != nullptr;
+  static const bool dbg_selfpub = debug_env("GCK_DEBUG_HIP_SELFPUB") != nullptr;
   const bool self_pub = !host_out && !w.b_chained && (!w.b_own_stream || aql_ok || dbg_selfpub);
   const uint32_t coherent = 0u;  // (results are published by the kernel end's write-back)
   // the join into the HSA queue when aql_ok and the code object has this variant
@@ -2858,8 +2858,8 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
 // GCK_DEBUG_BUNDLE: bundle 0's final query / join tables; GCK_DEBUG_TIMING: both stages'
 // per-bundle records appended to <prefix>.bin (kTimingWords u64 each).
 static void debug_dump(Engine& e, Workspace& w, uint32_t n) {
-  static const bool dbg_on = getenv("GCK_DEBUG_BUNDLE") != nullptr;
-  static const char* timing_env = getenv("GCK_DEBUG_TIMING");
+  static const bool dbg_on = debug_env("GCK_DEBUG_BUNDLE") != nullptr;
+  static const char* timing_env = debug_env("GCK_DEBUG_TIMING");
   if (dbg_on && w.dbg) {
     HIP_OK(hipDeviceSynchronize());
     const size_t dbg_words = 4 + kBQ * 6 + kBJ * 8;

@@ -2,6 +2,7 @@
 // device-resident snapshot + workspace. Everything behind the C ABI in include/gck.h.
 #pragma once
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <atomic>
@@ -18,6 +19,18 @@
 #include "gck_internal.hpp"
 
 namespace gck {
+
+// Diagnostic switches (GCK_DEBUG_*, GCK_STAGER_ANYWHERE): read from the environment only in the
+// debug build (make DEBUG=1 -> libgck_debug.so, -DGCK_DEBUG_KNOBS=1; load it with GCK_LIBRARY=...).
+// The product library ignores them: none changes a result, and none may change its timing.
+inline const char* debug_env(const char* name) {
+#if GCK_DEBUG_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 struct Error : std::runtime_error {
   int code;

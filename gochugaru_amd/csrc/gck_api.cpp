@@ -687,7 +687,7 @@ static void stager_place(int caller_cpu) {
 
 // The stager's thread: groups the queued batches in ticket order.
 static void stager_loop(gck_engine* ge, int caller_cpu) {
-  if (!getenv("GCK_STAGER_ANYWHERE")) stager_place(caller_cpu);
+  if (!debug_env("GCK_STAGER_ANYWHERE")) stager_place(caller_cpu);
   Engine& e = ge->impl;
   WatchStager& st = ge->stage;
   std::unique_lock<std::mutex> g(st.m);

@@ -1,6 +1,7 @@
 # The dispatch span of k_closure_join (config 4, device batches one at a time) under rocprofv3's
 # kernel trace, through HIP and through the engine's HSA queues with each fence / kernarg variant
 # (GCK_DEBUG_AQL_FENCE, GCK_DEBUG_AQL_HOSTARGS): attributes the AQL path's extra microseconds.
+# (the switches act in the debug build only: make -C gochugaru_amd/csrc DEBUG=1)
 #   bash tools/aql_span.sh <out dir> [tags]   (on the GPU box, from the repo root; tags: the variants to run)
 set -e
 OUT=$1
@@ -11,7 +12,7 @@ run() {
   local tag=$1
   shift
   if [ "$ONLY" != "  " ] && [[ "$ONLY" != *" $tag "* ]]; then return 0; fi
-  env "$@" timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/$tag" -o kt --output-format csv -- \
+  env GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so "$@" timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/$tag" -o kt --output-format csv -- \
     python3 tools/host_probe.py --phases device --lone 40 --batches 40 > "$OUT/$tag.json" 2> "$OUT/$tag.err"
   python3 - "$OUT/$tag" "$tag" <<'PY'
 import csv, sys, numpy as np

@@ -19,6 +19,8 @@
 #                                                        host-batch timeline (tools/host_probe.py), the
 #                                                        Watch grouping (tools/group_bench), the AQL span
 #                                                        attribution (tools/aql_span.sh)
+# (GCK_DEBUG_* switches act only in the debug build, make -C gochugaru_amd/csrc DEBUG=1 ->
+# gochugaru_amd/libgck_debug.so: the phases / mixed / pmcprobe jobs load it through GCK_LIBRARY)
 set -e
 CMD=$1
 TAG=$2
@@ -38,7 +40,7 @@ case "$CMD" in
     tail -c 600 "$OUT/bench.json"
     ;;
   phases)
-    GCK_DEBUG_PHASES=1 timeout -k 10 600 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
+    GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_PHASES=1 timeout -k 10 600 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
       || { tail -20 "$OUT/bench.err"; exit 1; }
     grep "\[gck" "$OUT/bench.err" | tail -20
     ;;
@@ -82,7 +84,7 @@ case "$CMD" in
     # a counter pass over the AQL path itself (the engine's own HSA queues), with the dispatch / wait
     # diagnostics of GCK_DEBUG_AQL on stderr; killed after 120 s if it stalls (run it last)
     SHORT="python3 bench.py --steps 20 --warmup 3 --no-oracle --no-cpu --host-steps 0 --inflight 1 $*"
-    GCK_DEBUG_AQL=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/aqlfetch" -o aqlfetch --output-format csv -- $SHORT > "$OUT/aqlfetch.json" 2> "$OUT/aqlfetch.err"
+    GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/aqlfetch" -o aqlfetch --output-format csv -- $SHORT > "$OUT/aqlfetch.json" 2> "$OUT/aqlfetch.err"
     rc=$?
     echo "pmc pass on the AQL path: status $rc"
     grep "gck aql" "$OUT/aqlfetch.err" | head -30 || true
@@ -112,7 +114,7 @@ case "$CMD" in
     tail -2 "$OUT/pytest.log"
     ;;
   mixed)
-    GCK_DEBUG_PHASES=1 timeout -k 10 400 python3 bench.py --config mixed "$@" > "$OUT/mixed.json" 2> "$OUT/mixed.err" \
+    GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_PHASES=1 timeout -k 10 400 python3 bench.py --config mixed "$@" > "$OUT/mixed.json" 2> "$OUT/mixed.err" \
       || { tail -20 "$OUT/mixed.err"; exit 1; }
     grep "gck watch\]\|gck apply\]\|gck relink\|gck group\|apply_publish" "$OUT/mixed.err" | tail -5
     ;;
