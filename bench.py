@@ -103,6 +103,9 @@ def parse():
                     help="strong scaling: a rank checks its slices of up to this many consecutive requests in one "
                          "dispatch (default 1: one dispatch per request slice, so `value` at N > 1 is strong scaling "
                          "of one 64K request; with N > 1 the figure at coalesce = N is reported as `coalesced`)")
+    ap.add_argument("--resident", type=int, default=0,
+                    help="1: the engine's resident closure join (GCK_FLAG_RESIDENT, resident.inc): requests are "
+                         "posted to one long-running launch instead of a dispatch each")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
     ap.add_argument("--watch-stage", type=int, default=1,
                     help="config 5: stage the next step's Watch batch (gck_watch_stage: grouped on the engine's "
@@ -428,7 +431,8 @@ def main():
                  bundle_checks=args.bundle_checks, bundle_frontier=args.bundle_frontier,
                  bundle_visited=args.bundle_visited, bundle_waves_per_cu=args.bundle_waves,
                  bundle_budget=args.bundle_budget, giant_slots=args.giant_slots,
-                 giant_stage=not args.no_giant, bidir=not args.no_bidir, bidir_both=args.bidir_both)
+                 giant_stage=not args.no_giant, bidir=not args.no_bidir, bidir_both=args.bidir_both,
+                 resident=bool(args.resident))
     if args.partitioned:
         eng.set_partition(rank, world)
     eng.load_schema(WL.schema)
@@ -1317,7 +1321,8 @@ def main():
                        "closure_checks_per_batch": round(st["closure_checks"] / n_batches, 1),
                        "slot_checks_per_batch": round(st["slot_checks"] / n_batches, 1),
                        "label_checks_per_batch": round(st["label_checks"] / n_batches, 1),
-                       "aql_dispatched_batches": int(st["aql_batches"])},
+                       "aql_dispatched_batches": int(st["aql_batches"]),
+                       "resident_batches": int(st["resident_batches"])},
             "setup_s": {"generate": round(t_gen, 1), "load": round(t_load, 1)},
             **({"timed_loop_ms": round(loop_s["s"] * 1e3, 4)} if loop_s["s"] is not None else {}),
             **({"loop_trace_us": {"submit_returned": [round(x * 1e6, 1) for x in trace[0::2]],

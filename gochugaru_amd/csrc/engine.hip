@@ -221,6 +221,9 @@ struct Workspace {
   bool b_aql = false;         // ... whose join was dispatched into the engine's HSA queue (aql.inc)
   uint32_t b_sum_blocks = 0;  // ... in that many blocks, each with a summary slot (closure.inc block_summary)
   bool b_validate = false;    // host items read in place: the join checks their context slots
+  bool b_res = false;         // ... posted to the resident join (resident.inc) instead
+  uint32_t ws_index = 0;      // the workspace's place in the pool (its resident-join slot)
+  uint32_t res_seq = 0;       // resident-join requests posted from it
   // ---- a uniform batch (gck_check_bulk_uniform / gck_check_submit_uniform) -----------------
   bool u_on = false;          // this batch is uniform: its wait packs the results (uniform_collect)
   bool u_join = false;        // ... and its join reads the pairs and writes the packed words in place
@@ -1503,8 +1506,12 @@ static void free_workspace(Workspace* w) {
 
 static void aql_drain(Engine& e);  // aql.inc
 static void aql_free(struct AqlState* st);
+static void res_free(Engine& e);   // resident.inc
+static uint32_t device_cus(int device);
 
 void device_free(Engine& e) {
+  res_free(e);   // (the resident join reads the snapshot and the workspaces: sealed, drained, freed)
+  e.res_tried = false;
   aql_drain(e);  // (dispatched joins read the snapshot: none may run past here)
   part_comm_free(e);
   if (e.delta_scratch) {
@@ -1639,6 +1646,7 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
 #include "bidir.inc"
 #include "labels.inc"
 #include "aql.inc"
+#include "resident.inc"
 
 // Builds the device snapshot from `csrs` and replaces e.dev with it. A CSR with `adopt` set
 // (delta re-link) is taken over without a copy, together with its index; bidir.inc reuses the
@@ -2055,13 +2063,22 @@ static size_t pool_cap(const Engine& e) { return e.cfg.workspaces ? e.cfg.worksp
 void ensure_pool(Engine& e) {
   if (e.part_world > 1) return;  // a partitioned engine runs on its own workspace (part_ws)
   std::lock_guard<std::mutex> lk(e.ws_mu);
-  while (e.ws_pool.size() < pool_cap(e)) e.ws_pool.push_back(create_workspace(e));
+  while (e.ws_pool.size() < pool_cap(e)) {
+    Workspace* w = create_workspace(e);
+    w->ws_index = (uint32_t)e.ws_pool.size();
+    e.ws_pool.push_back(w);
+  }
   if (!e.aql_tried) {
     e.aql_tried = true;
     e.aql = aql_init(e);
   }
   if (e.aql)
     for (Workspace* w : e.ws_pool) (void)aql_workspace(*e.aql, *w);  // (one without: its batches launch through HIP)
+  if (!e.res_tried) {
+    e.res_tried = true;
+    e.res = res_init(e);
+    res_start_keeper(e);
+  }
 }
 
 // `want` (1 or 2) free workspaces of the pool, taken together: a caller never holds one while it
@@ -2080,6 +2097,7 @@ void acquire_ws_n(Engine& e, int want, Workspace** out) {
       if (!w->busy && got.size() < need) got.push_back(w);
     while (got.size() < need && e.ws_pool.size() < cap) {
       Workspace* w = create_workspace(e);
+      w->ws_index = (uint32_t)e.ws_pool.size();
       e.ws_pool.push_back(w);
       got.push_back(w);
     }
@@ -2535,6 +2553,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
                       w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
                       ((aql_timed && e.aql->tick_hz) || !w.b_timed);
   w.b_aql = false;
+  w.b_res = false;
   w.b_sum_blocks = 0;
   // (GCK_DEBUG_HIP_SELFPUB: an engine-stream batch launched through HIP publishes itself from its
   // last block as an AQL-dispatched one does — the dispatch-span attribution of tools/aql_span.sh;
@@ -2674,7 +2693,13 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     // (half slots: the first 32 B of each resource slot, closure.inc HALF)
     if (fast && aql_ok && j.h_out && aql_kernel(e.aql, "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)"))
       aql_summaries(w, cj_args.j.coherent, cj_args.j.h_out, cj_args.j.done, cj_args.j.n_deferred, grid.x);
-    if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
+    // the resident join (resident.inc) takes the request without a dispatch of its own
+    const bool res_ok = fast && aql_ok && e.res && !w.b_timed && w.b_sum_blocks == grid.x &&
+                        (cj_args.j.coherent & kPubBySignal);
+    if (res_ok) {
+      aql_after_build(e);
+      res_post(e, w, cj_args.j, grid.x);
+    } else if (fast && aql_try("void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)", &cj_args,
                         sizeof(cj_args), grid.x)) {
     } else if (fast)
       hipExtLaunchKernelGGL((k_closure_join<24, kCjLdsBytesSmall, 32, true>), grid, block, 0, st, e0, e1, 0, c, j);
@@ -2703,7 +2728,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     HIP_OK(hipMemcpyAsync(w.b_xperm, d_perm, n, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
-  if (!w.b_aql && (!self_pub || !w.b_closure)) publish_launch(w, st);
+  if (!w.b_aql && !w.b_res && (!self_pub || !w.b_closure)) publish_launch(w, st);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
@@ -2714,7 +2739,8 @@ static void debug_dump(Engine& e, Workspace& w, uint32_t n);
 static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                             uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   if (w.b_aql) aql_wait(*e.aql, w);  // (the kernel has ended: its publication is complete)
-  if (w.b_aql && w.b_sum_blocks) aql_collect(w);
+  if (w.b_res) res_wait(e, w);       // (the resident join has finished the request's last chunk)
+  if ((w.b_aql || w.b_res) && w.b_sum_blocks) aql_collect(w);
   else wait_published(w, st, w.b_seq);
   add_counters(e, w, *w.h_ctr);
   w.ctr_clean = true;  // k_publish zeroed the device counters
@@ -2740,6 +2766,7 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     e.stats.slot_checks += n - n_cj - tasks;
     if (w.b_label) e.stats.label_checks += n - n_cj;
     if (w.b_aql) e.stats.aql_batches++;
+    if (w.b_res) e.stats.resident_batches++;
   }
   // recent batches with leftovers make the next ones chain their bundles on the device
   if (w.b_closure) {
@@ -3233,6 +3260,15 @@ static void copy_out(Workspace& w) {
 }
 
 void drain_batches(Engine& e) {
+  struct ResDrain {  // then the resident join (it reads the snapshot a writer is about to change)
+    Engine& e;
+    ~ResDrain() {
+      try {
+        res_drain(e);
+      } catch (const Error&) {
+      }
+    }
+  } res_drain_after{e};
   std::vector<Workspace*> busy;
   {
     std::lock_guard<std::mutex> lk(e.ws_mu);

@@ -234,6 +234,8 @@ struct Engine {
   void* patch_ev = nullptr;       // hipEvent_t: the last Watch publication's null-stream work, index patch included (make_ctx)
   void* build_ev = nullptr;       // hipEvent_t: the same publication's work before its index patch (the joins wait for it)
   uint64_t patch_seq = 0;         // publications recorded (0: none yet)
+  struct ResState* res = nullptr;  // the resident closure join (resident.inc; GCK_FLAG_RESIDENT)
+  bool res_tried = false;
   std::atomic<uint64_t> aql_patch_seen{0};  // the publication whose build the HSA-queue dispatches have waited for
   void* blob_host = nullptr;      // pinned: a Watch batch's program upload (device_build)
   size_t blob_host_cap = 0;

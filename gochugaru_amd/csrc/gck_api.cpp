@@ -216,7 +216,7 @@ struct WriterLock {
 };
 
 static_assert(sizeof(gck_config) == 88, "gck_config layout (include/gck.h) changed: bump GCK_ABI_VERSION");
-static_assert(sizeof(gck_stats) == 232, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
+static_assert(sizeof(gck_stats) == 240, "gck_stats layout (include/gck.h) changed: bump GCK_ABI_VERSION");
 static_assert(sizeof(gck_item) == 20 && sizeof(gck_tuple) == 32 && sizeof(gck_update) == 40, "item/tuple/update layout");
 
 int gck_abi_version(void) { return GCK_ABI_VERSION; }

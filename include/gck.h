@@ -124,6 +124,10 @@ extern "C" {
                                    closure join (saves ~128 B per user of HBM; slower) */
 #define GCK_FLAG_NO_LABELS 256u  /* gck_config.flags: no label-join stage (hub hierarchy labels and
                                     flattened resource slots; labels.inc) */
+#define GCK_FLAG_RESIDENT 512u  /* gck_config.flags: nested-group (closure-join) batches dispatched on the
+                                    engine's queues go to one resident launch per engine, whose
+                                    workgroups take 128-check chunks of the posted requests, instead of
+                                    a dispatch each (small requests: a 64K request sharded over GPUs) */
 #define GCK_FLAG_LAZY_CAVEATS 64u /* gck_config.flags: always evaluate check-time caveat contexts
                                      lazily (only the pairs a walk meets; by default a call whose
                                      partial instances x distinct contexts is small evaluates them all) */
@@ -234,6 +238,7 @@ typedef struct gck_stats {
   uint64_t aql_batches;        /* batches whose join the engine dispatched into its own HSA queue
                                   (engine-stream device batches, aql.inc) instead of launching it
                                   through HIP */
+  uint64_t resident_batches;   /* batches the resident join took (GCK_FLAG_RESIDENT) */
 } gck_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

@@ -45,7 +45,7 @@ def test_struct_layouts_match_header():
     assert E.TUPLE_DTYPE.itemsize == 32
     assert E.UPDATE_DTYPE.itemsize == 40
     assert C.sizeof(E._Config) == 88
-    assert C.sizeof(E._Stats) == 232
+    assert C.sizeof(E._Stats) == 240
     assert C.sizeof(E.Uniform) == 16
     assert E.ITEM_ERROR_DTYPE.itemsize == 8
     assert E.load_library().gck_abi_version() == 13
