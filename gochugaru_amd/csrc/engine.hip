@@ -143,6 +143,10 @@ struct DeviceSnapshot {
   // flattening of a resource visits is an ancestor of it): per vertex (pre, end), per type its
   // first vertex (kNone: not in the forest); null: no forest, a dirty subject's checks all defer
   uint32_t* lj_af = nullptr;
+  // the forest's parent edges (labels.inc lj_chain_walk): tupleset CSR << 32 | the parent's forest
+  // index (kNone: a root), per forest vertex; null: no chain programs
+  unsigned long long* lj_afp = nullptr;
+  uint32_t lj_afp_n = 0;
   std::vector<uint32_t> lj_af_base, lj_af_rows;
   std::vector<std::pair<uint32_t, uint16_t>> lj_dtype;  // direct-grant CSR -> the type of its rows
   // per dirty subject the forest intervals of the objects whose grants of it changed (kDovWords
@@ -1614,10 +1618,22 @@ void device_export(Engine& e, std::vector<HostCSR>& out) {
   }
 }
 
+static uint64_t mhash_slots(uint64_t ne) { return 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne)); }
+
+// Whether a plain direct-subject CSR of `ne` edges gets a membership index. Above 4 GB of index
+// (config 4's 1e9 group#member@user: 17.2 GB, a third of the snapshot) it is built only with
+// GCK_FLAG_BIG_MHASH: the one-round joins never probe it, and a check they leave tests membership
+// by a binary search of the row instead (member_test, the bundles' probes), as with
+// GCK_FLAG_NO_MHASH.
+static bool want_mhash(const Engine& e, uint64_t ne) {
+  if (ne == 0 || (e.cfg.flags & GCK_FLAG_NO_MHASH)) return false;
+  return mhash_slots(ne) * 8ull <= (4ull << 30) || (e.cfg.flags & GCK_FLAG_BIG_MHASH);
+}
+
 // Membership index of a plain CSR (d.off / d.nbr on the device): sets d.mhash, d.mmask and
 // d.has_wild.
 static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
-  const uint64_t slots = 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne));
+  const uint64_t slots = mhash_slots(ne);
   if (slots / kBucketKeys > (1ull << 32)) throw Error(GCK_E_CAPACITY, "membership index too large");
   unsigned long long* tab = dalloc<unsigned long long>(ds.allocs, slots, &ds.bytes);
   std::vector<void*> tmp;
@@ -1691,7 +1707,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
           b.mh_keys = h.mh_keys;
           adopted.push_back(const_cast<unsigned long long*>(h.dev_mhash));
           ds->bytes += (h.mmask + 1) * kBucketKeys * 8;
-        } else if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+        } else if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
         }
@@ -1705,7 +1721,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
         part_filter_device(e, *ds, h, d, ne);
         b.n_edges = ne;
         e.n_tuples -= std::min<uint64_t>(e.n_tuples, loaded - ne);  // (the engine counts what it holds)
-        if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+        if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
         }
@@ -1737,7 +1753,7 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
       }
       // hashed membership index for plain direct-subject kinds (the check
       // "is this subject in the row" becomes one probe instead of a binary search)
-      if (!h.ext && h.srel == kEllipsis && ne > 0 && !(e.cfg.flags & GCK_FLAG_NO_MHASH)) {
+      if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
         build_mhash(*ds, d, ne);
         b.mh_keys = ne;
       }
@@ -2587,6 +2603,10 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.o_meta = ds.lj_o_meta;
     j.dirty = ds.lj_dirty;
     j.dov = ds.lj_dov;
+    j.csrs = ds.csrs;
+    j.afp = ds.lj_afp;
+    j.n_csrs = ds.n_csrs;
+    j.afp_n = ds.lj_afp_n;
     bool cl = false;
     const bool cav = ds.lj_cav && w.cav_on;  // caveated pairs decided under the check contexts (cav_state)
     if (cav) {

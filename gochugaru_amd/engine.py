@@ -61,6 +61,7 @@ FLAG_LAZY_CAVEATS = 64
 FLAG_NO_SLOTS = 128
 FLAG_NO_LABELS = 256
 FLAG_RESIDENT = 512
+FLAG_BIG_MHASH = 1024
 SUBMIT_DEVICE = 1
 SUBMIT_ENGINE_STREAM = 2
 
@@ -366,13 +367,15 @@ class Engine:
                  membership_hash: bool = True, bundle_budget: int = 0, giant_frontier: int = 0,
                  giant_visited: int = 0, giant_slots: int = 0, giant_stage: bool = True,
                  bidir: bool = True, bidir_both: int = 0, workspaces: int = 0, closure: bool = True,
-                 lazy_caveats: bool = False, slots: bool = True, labels: bool = True, resident: bool = False):
+                 lazy_caveats: bool = False, slots: bool = True, labels: bool = True, resident: bool = False,
+                 big_membership_hash: bool = False):
         lib = load_library()
         flags = ((FLAG_PROFILE if profile else 0) | (FLAG_NO_BUNDLE if wide_only else 0)
                  | (0 if membership_hash else FLAG_NO_MHASH) | (0 if giant_stage else FLAG_NO_GIANT)
                  | (0 if bidir else FLAG_NO_BIDIR) | (0 if closure else FLAG_NO_CLOSURE)
                  | (FLAG_LAZY_CAVEATS if lazy_caveats else 0) | (0 if slots else FLAG_NO_SLOTS)
-                 | (0 if labels else FLAG_NO_LABELS) | (FLAG_RESIDENT if resident else 0))
+                 | (0 if labels else FLAG_NO_LABELS) | (FLAG_RESIDENT if resident else 0)
+                 | (FLAG_BIG_MHASH if big_membership_hash else 0))
         cfg = _Config(device, max_depth, max_batch, flags, visited_capacity, frontier_capacity,
                       segment_capacity, query_capacity, bundle_checks, bundle_frontier,
                       bundle_visited, bundle_waves_per_cu, bundle_budget, giant_frontier,

@@ -131,6 +131,9 @@ extern "C" {
 #define GCK_FLAG_LAZY_CAVEATS 64u /* gck_config.flags: always evaluate check-time caveat contexts
                                      lazily (only the pairs a walk meets; by default a call whose
                                      partial instances x distinct contexts is small evaluates them all) */
+#define GCK_FLAG_BIG_MHASH 1024u  /* gck_config.flags: build hashed membership indexes above 4 GB too
+                                     (by default a larger one is not built: the one-round joins never
+                                     read it, and the checks they leave binary-search the row) */
 
 typedef struct gck_engine gck_engine;
 

@@ -37,8 +37,11 @@ def test_config4_1e9_full_batch():
     assert e.tuple_count == G.n_tuples and G.n_tuples > 9e8
     gp, ge = run(e, items)
     st = e.stats()
+    footprint = e.device_bytes()
     e.close()
-    e2 = load_engine(G, closure=False)  # the wave-bundle search over the same batch
+    # the wave-bundle search over the same batch (with the membership index a default engine does
+    # not build above 4 GB: engine.hip want_mhash)
+    e2 = load_engine(G, closure=False, big_membership_hash=True)
     gp2, ge2 = run(e2, items)
     e2.close()
     _, prog, tab = _oracle(G)
@@ -50,6 +53,9 @@ def test_config4_1e9_full_batch():
     assert st["closure_checks"] == N  # every check answered by the closure join
     assert st["slot_checks"] > N // 2  # most from the user / resource slots alone
     assert 0.3 < np.mean(cp == 2) < 0.7
+    # the snapshot without the 17 GB membership index of group#member@user: <= 40 B per tuple
+    print(f"config 4 footprint: {footprint / 1e9:.1f} GB, {footprint / G.n_tuples:.1f} B per tuple")
+    assert footprint <= 40 * G.n_tuples, footprint
 
 
 def test_config4_1e9_partitioned_rccl_one_rank():

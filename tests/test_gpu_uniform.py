@@ -135,10 +135,11 @@ def test_uniform_chunks_above_max_batch():
 
 def test_uniform_compiled_loop():
     """gckd_run_uniform (the cgo caller's loop): 24 requests, 8 in flight, pinned buffers; every
-    request's words equal the oracle's."""
+    request's words equal the oracle's. (8 in flight from one thread needs 8 workspaces: a submit
+    waits for a free one, include/gck.h gck_config.workspaces.)"""
     schema, tuples, _ = gen.gdocs(6)
     rng = np.random.default_rng(9)
-    e = _engine(schema, tuples)
+    e = _engine(schema, tuples, workspaces=8)
     t_doc = e.type_id("doc")
     t_user = e.type_id("user")
     view = e.relation_id(t_doc, "view")
@@ -179,6 +180,9 @@ def test_evaluated_revision_across_a_watch_publication():
     e.apply_updates_text(2, f"CREATE {d}#viewer@{u}")
     perm, _ = b.wait()
     assert b.revision == 1 and int(perm[0]) == E.PERM_NO
+    # (interned again: the subject may be a name revision 1 did not hold — ABSENT in the request
+    # made then — which the update created; a caller interns each request's names)
+    items = e.make_items([parse_check(c)])
     perm, err, rev = e.check_bulk_at(items)
     assert rev == 2 and int(perm[0]) == E.PERM_HAS
     t_doc, t_user = e.type_id("doc"), e.type_id("user")

@@ -1,6 +1,7 @@
 # Round-6 GPU job: tests, then bench lines (each step under its own time limit; a failing step ends
 # the job). Usage on the GPU box (from the repo root): bash tools/r06_run.sh <tag> <step>...
-#   steps: tests | resident | bench64 | bench8k | bench16k | res64 | res8k | res16k | mixed | final
+#   steps: tests | chain | chunk | resident | bench64 | bench8k | bench16k | res64 | res8k | res16k | mixed |
+#          mixed2k | phases | pmc_nested | pmc_gdocs | pmc_github | pmc_mixed
 set -e
 TAG=$1
 shift
@@ -17,9 +18,23 @@ for step in "$@"; do
   case "$step" in
     tests)
       timeout -k 10 1000 python -u -m pytest tests/test_gpu_uniform.py tests/test_gpu_parity.py tests/test_gpu_hostpath.py \
-        tests/test_gpu_concurrency.py tests/test_gpu_partition.py tests/test_gpu_watch_fuzz.py -x -q --timeout 200 \
-        --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+        tests/test_gpu_concurrency.py tests/test_gpu_partition.py tests/test_gpu_watch_fuzz.py -x -v --timeout 120 \
+        --timeout-method thread --deselect tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch \
+        > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
       tail -2 "$OUT/pytest.log" ;;
+    chain)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_mixed.py tests/test_gpu_labels.py -x -v --timeout 300 \
+        --timeout-method thread > "$OUT/pytest_chain.log" 2>&1 || { tail -40 "$OUT/pytest_chain.log"; exit 1; }
+      tail -2 "$OUT/pytest_chain.log" ;;
+    chunkp)
+      timeout -k 10 150 python -u -m pytest tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s \
+        --timeout 100 --timeout-method thread > "$OUT/pytest_chunkp.log" 2>&1 || { tail -60 "$OUT/pytest_chunkp.log"; exit 1; }
+      tail -2 "$OUT/pytest_chunkp.log" ;;
+    chunk)
+      GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -k 10 150 python -u -m pytest \
+        tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s --timeout 100 --timeout-method thread \
+        > "$OUT/pytest_chunk.log" 2>&1 || { tail -60 "$OUT/pytest_chunk.log"; exit 1; }
+      tail -2 "$OUT/pytest_chunk.log" ;;
     resident)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread \
         > "$OUT/pytest_resident.log" 2>&1 || { tail -40 "$OUT/pytest_resident.log"; exit 1; }
@@ -31,6 +46,12 @@ for step in "$@"; do
     res8k) b res8k 400 --batch 8192 --steps 1000 --no-cpu --resident 1 ;;
     res16k) b res16k 400 --batch 16384 --steps 1000 --no-cpu --resident 1 ;;
     mixed) b mixed 400 --config mixed --steps 20 --warmup 5 ;;
+    mixed2k) b mixed2k 600 --config mixed --steps 2000 --no-cpu ;;
+    phases) bash tools/gpu.sh mixed "${TAG}_phases" --steps 200 --no-cpu ;;
+    pmc_nested) bash tools/gpu.sh profile "${TAG}_pmc_nested" ;;
+    pmc_gdocs) bash tools/gpu.sh profile "${TAG}_pmc_gdocs" --config gdocs ;;
+    pmc_github) bash tools/gpu.sh profile "${TAG}_pmc_github" --config github ;;
+    pmc_mixed) bash tools/gpu.sh profile "${TAG}_pmc_mixed" --config mixed ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
