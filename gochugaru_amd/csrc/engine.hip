@@ -1618,6 +1618,12 @@ void device_export(Engine& e, std::vector<HostCSR>& out) {
   }
 }
 
+void* pinned_alloc(size_t bytes) {
+  void* p = nullptr;
+  return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+void pinned_free(void* p) { (void)hipHostFree(p); }
+
 static uint64_t mhash_slots(uint64_t ne) { return 1ull << std::max<uint32_t>(10, ceil_log2(2 * ne)); }
 
 // Whether a plain direct-subject CSR of `ne` edges gets a membership index. Above 4 GB of index

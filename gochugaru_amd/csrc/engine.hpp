@@ -149,7 +149,18 @@ struct UpdateGroup {
   std::vector<uint8_t> is_ext;           // the upsert carries a caveat or an expiration
   std::vector<uint32_t> cav;             // caveat instance per key (0 = none)
   std::vector<int64_t> exp_us;           // expiration per key (0 = never)
+  // the merge's upload image of the group, laid out by group_updates (on the staging thread for a
+  // staged batch) in GroupBuffers::img: byte offsets of the keys, the insert flags of each class
+  // (plain, caveated / expiring), the caveats and the expirations; and the classes' summaries
+  const unsigned char* img = nullptr;
+  size_t o_keys = 0, o_ins[2] = {0, 0}, o_cav = 0, o_exp = 0;
+  uint32_t n_cand[2] = {0, 0}, max_row[2] = {0, 0};  // upserts into each class; 1 + their largest row
+  uint8_t wild_ins[2] = {0, 0}, wild_any = 0;       // a wildcard upserted into each class; any wildcard key
 };
+
+// Pinned host memory for the Watch upload images (engine.hip; null on failure).
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
 
 // snapshot.cpp group_updates' storage, reused batch after batch (a Watch batch holds it under the
 // writer lock): per kind its records, the bucket pass's buffers, and the groups it returns.
@@ -158,6 +169,15 @@ struct GroupBuffers {
   std::vector<uint64_t> tmp, kinds;
   std::vector<uint32_t> cnt, bucket;
   std::vector<UpdateGroup> out;
+  // the groups' upload image (pinned; the merge copies it to the device whole: delta.inc)
+  unsigned char* img = nullptr;
+  size_t img_cap = 0, img_bytes = 0;
+  GroupBuffers() = default;
+  GroupBuffers(const GroupBuffers&) = delete;
+  GroupBuffers& operator=(const GroupBuffers&) = delete;
+  ~GroupBuffers() {
+    if (img) pinned_free(img);
+  }
 };
 
 // The check-time caveat contexts of one call (CheckBulkPermissionsRequestItem.Context,

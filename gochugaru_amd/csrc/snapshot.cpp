@@ -549,6 +549,60 @@ const std::vector<UpdateGroup>& group_updates(const Engine& e, GroupBuffers& B, 
     g.exp_us.resize(w);
   }
   pc.mark("sort");
+  // the merge's upload image (delta.inc device_apply_build copies it to the device whole): per
+  // group its keys, the insert flags of its plain and its caveated class, caveats, expirations —
+  // made here, so that a staged batch's is made on the staging thread, beside the previous apply
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  size_t bytes = 0;
+  for (const UpdateGroup& g : out) {
+    const size_t m = g.keys.size();
+    bytes += al(8 * m) + 2 * al(m) + al(4 * m) + al(8 * m);
+  }
+  if (B.img_cap < bytes) {
+    if (B.img) pinned_free(B.img);
+    B.img = nullptr;
+    B.img_cap = 0;
+    const size_t cap = std::max(bytes + bytes / 2, (size_t)1 << 20);
+    B.img = static_cast<unsigned char*>(pinned_alloc(cap));
+    if (!B.img) throw Error(GCK_E_DEVICE, "pinned allocation of a Watch upload image failed");
+    B.img_cap = cap;
+  }
+  B.img_bytes = bytes;
+  size_t at = 0;
+  for (UpdateGroup& g : out) {
+    const size_t m = g.keys.size();
+    g.img = B.img;
+    g.o_keys = at, at += al(8 * m);
+    g.o_ins[0] = at, at += al(m);
+    g.o_ins[1] = at, at += al(m);
+    g.o_cav = at, at += al(4 * m);
+    g.o_exp = at, at += al(8 * m);
+    std::memcpy(B.img + g.o_keys, g.keys.data(), 8 * m);
+    std::memcpy(B.img + g.o_cav, g.cav.data(), 4 * m);
+    std::memcpy(B.img + g.o_exp, g.exp_us.data(), 8 * m);
+    uint8_t* i0 = B.img + g.o_ins[0];
+    uint8_t* i1 = B.img + g.o_ins[1];
+    // (branch-free: the upsert / caveat mix of a Watch batch is random)
+    uint32_t nc0 = 0, nc1 = 0, mr0 = 0, mr1 = 0, w0 = 0, w1 = 0, wa = 0;
+    for (size_t d = 0; d < m; ++d) {
+      const uint32_t up = g.upsert[d] != 0, x = g.is_ext[d] != 0;
+      const uint32_t in1 = up & x, in0 = up & (x ^ 1u);
+      const uint32_t row1 = (uint32_t)(g.keys[d] >> 32) + 1, w = (uint32_t)g.keys[d] == kWildcard;
+      i0[d] = (uint8_t)in0;
+      i1[d] = (uint8_t)in1;
+      nc0 += in0;
+      nc1 += in1;
+      mr0 = std::max(mr0, in0 ? row1 : 0u);
+      mr1 = std::max(mr1, in1 ? row1 : 0u);
+      w0 |= in0 & w;
+      w1 |= in1 & w;
+      wa |= w;
+    }
+    g.n_cand[0] = nc0, g.n_cand[1] = nc1;
+    g.max_row[0] = mr0, g.max_row[1] = mr1;
+    g.wild_ins[0] = (uint8_t)w0, g.wild_ins[1] = (uint8_t)w1, g.wild_any = (uint8_t)wa;
+  }
+  pc.mark("image");
   return out;
 }
 
