@@ -107,9 +107,10 @@ def parse():
                     help="1: the engine's resident closure join (GCK_FLAG_RESIDENT, resident.inc): requests are "
                          "posted to one long-running launch instead of a dispatch each")
     ap.add_argument("--churn", type=float, default=0.001, help="config 5: updates per step, as a fraction of tuples")
-    ap.add_argument("--watch-stage", type=int, default=1,
-                    help="config 5: stage the next step's Watch batch (gck_watch_stage: grouped on the engine's "
-                         "thread) while the step applies its own; 0 = gck_apply_updates")
+    ap.add_argument("--watch-stage", type=int, default=2,
+                    help="config 5: Watch batches staged ahead of the one a step applies (gck_watch_stage: grouped "
+                         "on the engine's staging threads beside the apply; a consumer holding that many further "
+                         "responses); 0 = gck_apply_updates")
     ap.add_argument("--scale", type=float, default=1.0, help="configs 2 / 3: 1.0 = 10M / 100M tuples")
     args = ap.parse_args()
     nested = args.config == "nested"
@@ -493,7 +494,7 @@ def main():
         from gochugaru_amd.engine import Contexts
         n_up = max(1, int(n_tuples * args.churn))
         batches = [WL.M.churn(n_up, WL.cav) for _ in range(args.warm + args.steps)]
-        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "pending": None, "ticket": None}
+        rev = {"r": 1, "k": 0, "apply_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "pending": None, "tq": []}
         m_ctx = Contexts(CONTEXTS)
 
         def step():
@@ -501,16 +502,16 @@ def main():
             rev["r"] += 1
             k = rev["k"]
             if args.watch_stage:
-                # a Watch consumer holding the next batch stages it (the engine's thread validates
-                # and groups it) before it applies this one: every step still groups, merges and
-                # publishes one whole batch, the next batch's grouping beside this one's merge
-                if rev["ticket"] is None:
-                    rev["ticket"] = eng.stage_updates(batches[k])
-                # (the last step stages its own batch again, discarded after the run: every timed
-                # step stages one batch, so the timed region holds as many groupings as applies)
-                nxt = eng.stage_updates(batches[min(k + 1, len(batches) - 1)])
-                eng.apply_staged(rev["r"], rev["ticket"])
-                rev["ticket"] = nxt
+                # a Watch consumer holding the next `watch_stage` responses stages them (the
+                # engine's staging threads validate and group them) before it applies this one:
+                # every step still groups, merges and publishes one whole batch, the later batches'
+                # grouping beside this one's merge. After the first step each step stages exactly
+                # one batch (the last steps stage the final batch again, discarded after the run),
+                # so the timed region holds as many groupings as applies
+                tq = rev["tq"]
+                while len(tq) < args.watch_stage + 1:
+                    tq.append(eng.stage_updates(batches[min(k + len(tq), len(batches) - 1)]))
+                eng.apply_staged(rev["r"], tq.pop(0))
             else:
                 eng.apply_updates(rev["r"], batches[k])
             rev["k"] += 1
@@ -531,9 +532,10 @@ def main():
             if rev["pending"] is not None:
                 rev["pending"].wait()
                 rev["pending"] = None
-            if rev["ticket"] is not None and rev["k"] >= len(batches):
-                eng.discard_staged(rev["ticket"])
-                rev["ticket"] = None
+            if rev["k"] >= len(batches):
+                for t in rev["tq"]:
+                    eng.discard_staged(t)
+                rev["tq"] = []
     elif WL.kind == "quota":
         # per step one batch with its own 64K contexts (pre-generated, rotated): the contexts are
         # parsed, the walk records the (instance, context) pairs it meets, the host evaluates
@@ -1336,12 +1338,13 @@ def main():
                           "check_submit_ms_per_step": round(rev["submit_timed"] / args.steps * 1e3, 3),
                           "check_wait_ms_per_step": round(rev["wait_timed"] / args.steps * 1e3, 3),
                           "revision": rev["r"],
-                          "staged": bool(args.watch_stage),
-                          "staging": ("gck_watch_stage: each step stages the next Watch batch (validated and grouped "
-                                      "on the engine's thread) and then applies its own (gck_watch_apply_staged: "
-                                      "merge, re-link, publication); the grouping of step k+1 runs beside step k's "
-                                      "device work" if args.watch_stage else "gck_apply_updates: grouping inside the "
-                                      "apply")}} if WL.kind == "mixed" else {}),
+                          "staged": int(args.watch_stage),
+                          "staging": (f"gck_watch_stage: each step stages the Watch batch {args.watch_stage} ahead "
+                                      "(validated and grouped, its upload image laid out, on the engine's two "
+                                      "staging threads) and then applies its own (gck_watch_apply_staged: merge, "
+                                      "re-link, publication); the later batches' grouping runs beside this step's "
+                                      "apply and device work" if args.watch_stage else "gck_apply_updates: grouping "
+                                      "inside the apply")}} if WL.kind == "mixed" else {}),
             **({"check_stage": check_stage} if check_stage else {}),
         }
         print(json.dumps(line), flush=True)

@@ -148,7 +148,7 @@ struct WatchStager {
     const gck_update* ups = nullptr;
     size_t n = 0;
     uint64_t ticket = 0;  // 0: free
-    int state = 0;        // 1 queued, 2 grouped (or failed)
+    int state = 0;        // 1 queued, 3 being grouped, 2 grouped (or failed)
     bool ok = false;
     uint64_t gen = 0;
     std::vector<gck_update> mine;  // (a partitioned rank's own updates)
@@ -157,17 +157,20 @@ struct WatchStager {
   } slots[kSlots];
   std::mutex m;
   std::condition_variable cv_job, cv_done;
-  std::thread th;
+  // two threads: a consumer holding the next two responses has both grouped beside its apply (the
+  // grouping of one config-5 batch takes about as long as an apply, ~80-100 us)
+  static constexpr int kThreads = 2;
+  std::thread th[kThreads];
   bool stop = false;
   uint64_t next_ticket = 1;
   ~WatchStager() {
-    if (!th.joinable()) return;
     {
       std::lock_guard<std::mutex> g(m);
       stop = true;
     }
     cv_job.notify_all();
-    th.join();
+    for (std::thread& t : th)
+      if (t.joinable()) t.join();
   }
 };
 
@@ -700,6 +703,7 @@ static void stager_loop(gck_engine* ge, int caller_cpu) {
       st.cv_job.wait(g);
     }
     if (!s) return;
+    s->state = 3;  // (the other thread takes the next queued one)
     const gck_update* ups = s->ups;
     size_t n = s->n;
     g.unlock();
@@ -753,7 +757,8 @@ int gck_watch_stage(gck_engine* ge, const gck_update* updates, size_t n, uint64_
         break;
       }
     REQUIRE(s, GCK_E_CAPACITY, "every staging slot holds a batch: apply or discard one first");
-    if (!st.th.joinable()) st.th = std::thread(stager_loop, ge, sched_getcpu());
+    for (std::thread& t : st.th)
+      if (!t.joinable()) t = std::thread(stager_loop, ge, sched_getcpu());
     s->ups = updates;
     s->n = n;
     s->ticket = st.next_ticket++;

@@ -19,7 +19,7 @@ for step in "$@"; do
     tests)
       timeout -k 10 1000 python -u -m pytest tests/test_gpu_uniform.py tests/test_gpu_parity.py tests/test_gpu_hostpath.py \
         tests/test_gpu_concurrency.py tests/test_gpu_partition.py tests/test_gpu_watch_fuzz.py -x -v --timeout 120 \
-        --timeout-method thread --deselect tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch \
+        --timeout-method thread \
         > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
       tail -2 "$OUT/pytest.log" ;;
     chain)
@@ -52,6 +52,17 @@ for step in "$@"; do
     pmc_gdocs) bash tools/gpu.sh profile "${TAG}_pmc_gdocs" --config gdocs ;;
     pmc_github) bash tools/gpu.sh profile "${TAG}_pmc_github" --config github ;;
     pmc_mixed) bash tools/gpu.sh profile "${TAG}_pmc_mixed" --config mixed ;;
+    part) b part 600 --partitioned --steps 100 --warmup 5 --no-cpu ;;
+    partkt)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/part_kt" -o kt --output-format csv -- \
+        python3 bench.py --partitioned --steps 100 --warmup 5 --no-cpu --no-oracle > "$OUT/part_kt.json" 2> "$OUT/part_kt.err" \
+        || { tail -20 "$OUT/part_kt.err"; exit 1; }
+      find "$OUT/part_kt" -name "*kernel_trace.csv" -delete
+      find "$OUT/part_kt" -name "*agent_info.csv" -delete ;;
+    full)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_full.log" 2>&1 || { tail -40 "$OUT/pytest_full.log"; exit 1; }
+      tail -2 "$OUT/pytest_full.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
