@@ -275,7 +275,8 @@ struct Engine {
   size_t recycle_bytes = 0;
   gck_stats stats{};
   // batches to come that chain the wave bundles behind the join in stage A (engine.hip
-  // bundles_launch): reset to 16 by a batch whose join left checks, counted down by one that left none
+  // bundles_launch): reset to 16 by a batch whose join left kChainLeftovers or more, counted down by
+  // one that left fewer
   std::atomic<int> defer_recent{0};
   // direct AQL dispatch of the join kernels (engine.hip aql.inc): the engine's HSA queue and the
   // kernels of libgck_kernels.co, set up at the first snapshot (null: launches go through HIP)
