@@ -2613,6 +2613,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.afp = ds.lj_afp;
     j.n_csrs = ds.n_csrs;
     j.afp_n = ds.lj_afp_n;
+    j.cav_static = ds.cav_static;
     bool cl = false;
     const bool cav = ds.lj_cav && w.cav_on;  // caveated pairs decided under the check contexts (cav_state)
     if (cav) {
@@ -2722,6 +2723,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     // the resident join (resident.inc) takes the request without a dispatch of its own
     const bool res_ok = fast && aql_ok && e.res && !w.b_timed && w.b_sum_blocks == grid.x &&
                         (cj_args.j.coherent & kPubBySignal);
+    static const bool dbg_res = debug_env("GCK_DEBUG_RES") != nullptr;  // (why a batch did not go resident)
+    if (dbg_res && e.res && !res_ok)
+      std::fprintf(stderr, "[gck res] not resident: fast=%d aql_ok=%d own=%d host_out=%d chained=%d clean=%d cav=%d timed=%d sum=%u/%u pub=%u\n",
+                   (int)fast, (int)aql_ok, (int)w.b_own_stream, (int)host_out, (int)w.b_chained, (int)ctr_was_clean,
+                   (int)w.cav_on, (int)w.b_timed, w.b_sum_blocks, grid.x, cj_args.j.coherent);
     if (res_ok) {
       aql_after_build(e);
       res_post(e, w, cj_args.j, grid.x);

@@ -30,6 +30,10 @@ for step in "$@"; do
       timeout -k 10 150 python -u -m pytest tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s \
         --timeout 100 --timeout-method thread > "$OUT/pytest_chunkp.log" 2>&1 || { tail -60 "$OUT/pytest_chunkp.log"; exit 1; }
       tail -2 "$OUT/pytest_chunkp.log" ;;
+    resdbg)
+      GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_RES=1 timeout -k 10 300 python -u -m pytest \
+        tests/test_gpu_resident.py -x -v -s --timeout 120 --timeout-method thread > "$OUT/pytest_resdbg.log" 2>&1
+      echo "resdbg rc=$?"; grep "gck res" "$OUT/pytest_resdbg.log" | sort | uniq -c | sort -rn | head -8; tail -2 "$OUT/pytest_resdbg.log" ;;
     chunk)
       GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -k 10 150 python -u -m pytest \
         tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s --timeout 100 --timeout-method thread \
