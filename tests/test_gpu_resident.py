@@ -29,7 +29,10 @@ def _setup(seed=3, **kw):
     return e, schema, tuples
 
 
-def _random_checks(rng, n, n_docs=305, n_users=605):
+def _random_checks(rng, n, n_docs=300, n_users=600):
+    # (names the snapshot holds: a request with unknown names leaves its checks to the bundles —
+    # 2-3 % of 8,192 here — and a batch leaving 32 or more has the next 16 chained behind their joins
+    # on a HIP stream, engine.hip kChainLeftovers, which is not the resident launch)
     return [f"doc:d{rng.integers(0, n_docs)}#view@user:u{rng.integers(0, n_users)}" for _ in range(n)]
 
 

@@ -34,6 +34,11 @@ for step in "$@"; do
       GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_RES=1 timeout -k 10 300 python -u -m pytest \
         tests/test_gpu_resident.py -x -v -s --timeout 120 --timeout-method thread > "$OUT/pytest_resdbg.log" 2>&1
       echo "resdbg rc=$?"; grep "gck res" "$OUT/pytest_resdbg.log" | sort | uniq -c | sort -rn | head -8; tail -2 "$OUT/pytest_resdbg.log" ;;
+    watch)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_delta.py tests/test_gpu_watch_fuzz.py tests/test_gpu_watch_nested.py \
+        tests/test_gpu_watch_concurrent.py tests/test_gpu_resident.py -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_watch.log" 2>&1 || { tail -40 "$OUT/pytest_watch.log"; exit 1; }
+      tail -2 "$OUT/pytest_watch.log" ;;
     chunk)
       GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -k 10 150 python -u -m pytest \
         tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s --timeout 100 --timeout-method thread \
