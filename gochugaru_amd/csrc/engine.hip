@@ -147,6 +147,7 @@ struct DeviceSnapshot {
   // index (kNone: a root), per forest vertex; null: no chain programs
   unsigned long long* lj_afp = nullptr;
   uint32_t lj_afp_n = 0;
+  uint32_t* lj_anc = nullptr;  // per forest vertex its ancestors, kAncWords each (labels.inc lj_chain_wave)
   std::vector<uint32_t> lj_af_base, lj_af_rows;
   std::vector<std::pair<uint32_t, uint16_t>> lj_dtype;  // direct-grant CSR -> the type of its rows
   // per dirty subject the forest intervals of the objects whose grants of it changed (kDovWords
@@ -2555,7 +2556,9 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // list's length on the device — no host round trip in the wait — when recent batches of the
   // engine left checks (a persistent bundle launch over an empty list costs a few microseconds,
   // the round trip tens; engine.hpp Engine::defer_recent)
-  w.b_chained = w.b_closure && e.defer_recent.load(std::memory_order_relaxed) > 0;
+  // (not with the resident join: its requests are posted to the running launch, and what they
+  // leave is bundled after the wait like an AQL-dispatched join's)
+  w.b_chained = w.b_closure && e.defer_recent.load(std::memory_order_relaxed) > 0 && !e.res;
   // the join publishes the batch itself unless something must follow it first: a host batch's
   // copies, the chained bundles, or — for a device batch on the engine's stream, whose caller has
   // no stream to order its reads after the kernel's end — the end-of-kernel L2 write-back
@@ -2614,6 +2617,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     j.n_csrs = ds.n_csrs;
     j.afp_n = ds.lj_afp_n;
     j.cav_static = ds.cav_static;
+    j.anc = ds.lj_anc;
     bool cl = false;
     const bool cav = ds.lj_cav && w.cav_on;  // caveated pairs decided under the check contexts (cav_state)
     if (cav) {
@@ -2761,6 +2765,11 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
     HIP_OK(hipMemcpyAsync(w.b_xerr, d_err, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   }
   if (!w.b_aql && !w.b_res && (!self_pub || !w.b_closure)) publish_launch(w, st);
+  static const bool dbg_res_any = debug_env("GCK_DEBUG_RES") != nullptr;
+  if (dbg_res_any && e.res && !w.b_res)
+    std::fprintf(stderr, "[gck res] batch n=%u not resident: lj=%d cj=%d aql_ok=%d aql=%d chained=%d clean=%d own=%d host_out=%d\n",
+                 n, (int)lj, (int)cj, (int)aql_ok, (int)w.b_aql, (int)w.b_chained, (int)ctr_was_clean,
+                 (int)w.b_own_stream, (int)host_out);
 }
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);

@@ -16,14 +16,14 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 # demangled name (as aql.inc looks it up) -> sizes of the by-value parameters
 KERNELS = {
-    "void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)": [240],
-    "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)": [240],
-    "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)": [240],
-    "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)": [240],
-    "void gck::k_label_join<24, 16u, 32u, true>(gck::LjArgs)": [240],
-    "void gck::k_label_join<24, 32u, 32u, true>(gck::LjArgs)": [240],
-    "void gck::k_label_join<32, 16u, 32u, true>(gck::LjArgs)": [240],
-    "void gck::k_label_join<32, 32u, 32u, true>(gck::LjArgs)": [240],
+    "void gck::k_label_join<24, 16u, 32u, false>(gck::LjArgs)": [248],
+    "void gck::k_label_join<24, 32u, 32u, false>(gck::LjArgs)": [248],
+    "void gck::k_label_join<32, 16u, 32u, false>(gck::LjArgs)": [248],
+    "void gck::k_label_join<32, 32u, 32u, false>(gck::LjArgs)": [248],
+    "void gck::k_label_join<24, 16u, 32u, true>(gck::LjArgs)": [248],
+    "void gck::k_label_join<24, 32u, 32u, true>(gck::LjArgs)": [248],
+    "void gck::k_label_join<32, 16u, 32u, true>(gck::LjArgs)": [248],
+    "void gck::k_label_join<32, 32u, 32u, true>(gck::LjArgs)": [248],
     "void gck::k_closure_join<24, 2048u, 32u, true>(gck::Ctx, gck::CjArgs)": [344, 184],
 }
 
