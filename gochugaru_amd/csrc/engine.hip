@@ -1632,10 +1632,15 @@ static uint64_t mhash_slots(uint64_t ne) { return 1ull << std::max<uint32_t>(10,
 // GCK_FLAG_BIG_MHASH: the one-round joins never probe it, and a check they leave tests membership
 // by a binary search of the row instead (member_test, the bundles' probes), as with
 // GCK_FLAG_NO_MHASH.
-static bool want_mhash(const Engine& e, uint64_t ne) {
-  if (ne == 0 || (e.cfg.flags & GCK_FLAG_NO_MHASH)) return false;
+static bool mhash_affordable(const Engine& e, uint64_t ne) {
   return mhash_slots(ne) * 8ull <= (4ull << 30) || (e.cfg.flags & GCK_FLAG_BIG_MHASH);
 }
+static bool want_mhash(const Engine& e, uint64_t ne) {
+  if (ne == 0 || (e.cfg.flags & GCK_FLAG_NO_MHASH)) return false;
+  return mhash_affordable(e, ne);
+}
+// DevCSR::pad bit: has_wild is known although the CSR has no index (scan_wild)
+constexpr uint16_t kCsrWildKnown = 1;
 
 // Membership index of a plain CSR (d.off / d.nbr on the device): sets d.mhash, d.mmask and
 // d.has_wild.
@@ -1662,6 +1667,34 @@ static void build_mhash(DeviceSnapshot& ds, DevCSR& d, uint64_t ne) {
   d.mhash = tab;
   d.mmask = slots / kBucketKeys - 1;
   d.has_wild = hw ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_wild(const uint32_t* __restrict__ nbr, unsigned long long n,
+                                                      unsigned* __restrict__ flag) {
+  const unsigned long long e = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  if (e < n && nbr[e] == kWildcard) *flag = 1u;
+}
+
+// has_wild of a plain direct CSR that gets no index because of its size (want_mhash): the closure
+// join's and the bidirectional search's planning read it (bidir.inc) as they read an index's.
+static void scan_wild(const Engine& e, DevCSR& d, uint64_t ne) {
+  if (ne == 0 || (e.cfg.flags & GCK_FLAG_NO_MHASH) || mhash_affordable(e, ne)) return;
+  std::vector<void*> tmp;
+  unsigned hw = 0;
+  try {
+    unsigned* flag = dalloc<unsigned>(tmp, 1);
+    HIP_OK(hipMemsetAsync(flag, 0, 4, nullptr));
+    hipLaunchKernelGGL(k_scan_wild, dim3((uint32_t)((ne + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0, d.nbr,
+                       (unsigned long long)ne, flag);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpy(&hw, flag, 4, hipMemcpyDeviceToHost));
+  } catch (...) {
+    free_list(tmp);
+    throw;
+  }
+  free_list(tmp);
+  d.has_wild = hw ? 1 : 0;
+  d.pad |= kCsrWildKnown;
 }
 
 #include "heights.inc"
@@ -1717,6 +1750,11 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
         } else if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
+        } else if (!h.ext && h.srel == kEllipsis && h.wild_known) {
+          d.has_wild = h.has_wild;  // (an index-less CSR taken over or merged: its wildcard flag carried over)
+          d.pad |= kCsrWildKnown;
+        } else if (!h.ext && h.srel == kEllipsis) {
+          scan_wild(e, d, ne);
         }
         table.push_back(d);
         info.push_back({ne, h.stype});
@@ -1731,6 +1769,8 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
         if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
           build_mhash(*ds, d, ne);
           b.mh_keys = ne;
+        } else if (!h.ext && h.srel == kEllipsis) {
+          scan_wild(e, d, ne);
         }
         table.push_back(d);
         info.push_back({ne, h.stype});
@@ -1763,6 +1803,8 @@ static DeviceSnapshot* device_build(Engine& e, std::vector<HostCSR>& csrs, bool 
       if (!h.ext && h.srel == kEllipsis && want_mhash(e, ne)) {
         build_mhash(*ds, d, ne);
         b.mh_keys = ne;
+      } else if (!h.ext && h.srel == kEllipsis) {
+        scan_wild(e, d, ne);
       }
       table.push_back(d);
       info.push_back({ne, h.stype});

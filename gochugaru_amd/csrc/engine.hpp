@@ -137,6 +137,7 @@ struct HostCSR {
   const unsigned long long* dev_mhash = nullptr;  // nullptr: build the index if the kind has one
   unsigned long long mmask = 0;
   uint8_t has_wild = 0;
+  uint8_t wild_known = 0;  // has_wild holds without dev_mhash (engine.hip scan_wild's result, carried over)
   uint64_t mh_keys = 0;  // keys + tombstones in dev_mhash
 };
 

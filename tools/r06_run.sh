@@ -39,6 +39,10 @@ for step in "$@"; do
         tests/test_gpu_watch_concurrent.py tests/test_gpu_resident.py -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_watch.log" 2>&1 || { tail -40 "$OUT/pytest_watch.log"; exit 1; }
       tail -2 "$OUT/pytest_watch.log" ;;
+    fs4)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_fullsize.py -k "config4_1e9_full_batch" -x -v -s --timeout 800 \
+        --timeout-method thread > "$OUT/pytest_fs4.log" 2>&1 || { tail -40 "$OUT/pytest_fs4.log"; exit 1; }
+      grep "footprint" "$OUT/pytest_fs4.log"; tail -2 "$OUT/pytest_fs4.log" ;;
     chunk)
       GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -k 10 150 python -u -m pytest \
         tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s --timeout 100 --timeout-method thread \
