@@ -37,7 +37,7 @@ def test_config4_1e9_full_batch():
     assert e.tuple_count == G.n_tuples and G.n_tuples > 9e8
     gp, ge = run(e, items)
     st = e.stats()
-    footprint = e.device_bytes()
+    footprint = e.device_bytes
     e.close()
     # the wave-bundle search over the same batch (with the membership index a default engine does
     # not build above 4 GB: engine.hip want_mhash)
