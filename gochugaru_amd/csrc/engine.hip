@@ -2816,7 +2816,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
 
 static void debug_dump(Engine& e, Workspace& w, uint32_t n);
 
-constexpr uint32_t kChainLeftovers = 32;  // leftovers of a batch that make the next 16 chain their bundles
+constexpr uint32_t kChainLeftovers = 1;  // leftovers of a batch that make the next 16 chain their bundles
 
 // Stages B and C of a bundle batch after stage A was published: the checks stage A deferred
 // (giant, or rooted high enough to need exact depth) through the workgroup bundles and/or the
@@ -2853,11 +2853,10 @@ static float bundles_finish(Engine& e, Workspace& w, const gck_item* d_items, ui
     if (w.b_aql) e.stats.aql_batches++;
     if (w.b_res) e.stats.resident_batches++;
   }
-  // recent batches with many leftovers make the next ones chain their bundles on the device. A
-  // few leftovers now and then (config 5 since the chain walk: ~0.4 per batch, where round 5 had
-  // 55-1,100) are cheaper finished here, behind the join's own dispatch into the engine's queues,
-  // than every batch launched through HIP with a persistent bundle launch behind it (the chained
-  // path: 109 us per config-5 check batch against its 24 us join)
+  // recent batches with leftovers make the next ones chain their bundles on the device (config 5
+  // since the chain walk leaves ~0.4 per batch — documents whose own wildcard grant a Watch batch
+  // changed — in ~70 % of its batches: chained, 419 M checks/s; finished here after the join's
+  // own dispatch, 351-375 M, the bundles' launch and round trip inside the next publication)
   if (w.b_closure) {
     if (n_cj >= kChainLeftovers) e.defer_recent.store(16, std::memory_order_relaxed);
     else if (e.defer_recent.load(std::memory_order_relaxed) > 0) e.defer_recent.fetch_sub(1, std::memory_order_relaxed);

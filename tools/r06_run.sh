@@ -43,6 +43,15 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests/test_gpu_fullsize.py -k "config4_1e9_full_batch" -x -v -s --timeout 800 \
         --timeout-method thread > "$OUT/pytest_fs4.log" 2>&1 || { tail -40 "$OUT/pytest_fs4.log"; exit 1; }
       grep "footprint" "$OUT/pytest_fs4.log"; tail -2 "$OUT/pytest_fs4.log" ;;
+    ljtime) timeout -k 10 400 bash tools/timing_lj.sh "$OUT/ljt" --config mixed ;;
+    qsweep)  # 8,192-check requests: queues x requests in flight (the debug library's queue-count switch)
+      for qi in "4 16" "8 16" "8 32"; do
+        set -- $qi
+        GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL_QUEUES=$1 timeout -k 10 300 python3 bench.py \
+          --batch 8192 --steps 1000 --inflight $2 --no-cpu --no-oracle --host-steps 0 > "$OUT/q$1_if$2.json" 2> "$OUT/q$1_if$2.err" \
+          || { tail -5 "$OUT/q$1_if$2.err"; exit 1; }
+        echo "queues=$1 inflight=$2 $(python3 -c "import json; print(json.load(open('$OUT/q$1_if$2.json'))['value'])")"
+      done ;;
     chunk)
       GCK_LIBRARY=$PWD/gochugaru_amd/libgck_debug.so GCK_DEBUG_AQL=1 timeout -k 10 150 python -u -m pytest \
         tests/test_gpu_uniform.py::test_uniform_chunks_above_max_batch -x -v -s --timeout 100 --timeout-method thread \
