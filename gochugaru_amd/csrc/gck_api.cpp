@@ -182,8 +182,8 @@ struct gck_engine {
 template <class F>
 static int guard(F&& f) {
   try {
-    f();
-    g_last_error.clear();
+    f();  // (a success leaves the message of the thread's last failure, as errno: a caller's loop that
+          // drains its batches after an error still reads that error's message)
     return GCK_OK;
   } catch (const Error& ex) {
     g_last_error = ex.what();

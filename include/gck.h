@@ -50,7 +50,8 @@
  * pointer after a call returns, except that gck_check_submit keeps the output pointers (and, for
  * device batches or host items in gck_host_alloc memory, the item pointer) until the matching
  * gck_check_wait. Return value: GCK_OK (0)
- * or a negative GCK_E_* status; the message is available from gck_last_error() (thread-local).
+ * or a negative GCK_E_* status; the message is available from gck_last_error() (thread-local; the
+ * message of the thread's last failure — a later success leaves it, as errno).
  * Threading: gck_check_bulk*, gck_check_submit / gck_check_wait and the lookups may be called
  * concurrently from any number of threads: each batch in flight runs on its own pooled
  * workspace and HIP stream (gck_config.workspaces of them; a call waits for a free one).

@@ -184,6 +184,53 @@ def test_overlay_hits_decided_by_the_chain_walk():
     e.close()
 
 
+def _wild_checks(M, ups, rng, per=8):
+    """Checks of the documents whose wildcard grant (doc#viewer@user:*) a Watch batch touched or
+    deleted, each against `per` random users, view and edit, with a random context slot."""
+    W = M.W
+    t = ups["tuple"]
+    docs = np.unique(t["resource_id"][(t["subject_id"] == S.WILD) & (t["resource_type"] == W.t("doc"))])
+    n = len(docs) * per
+    items = np.zeros((n, 5), np.int64)
+    for k in range(n):
+        perm = ("view", "edit")[int(rng.integers(0, 2))]
+        items[k] = [W.t("doc") | (W.r("doc", perm) << 16), int(docs[k // per]), W.t("user") | (S.ELLIPSIS << 16),
+                    int(rng.integers(0, W.counts["user"])), int(rng.integers(0, 3))]
+    items = items - ((items >= 2 ** 31).astype(np.int64) << 32)
+    return len(docs), torch.from_numpy(items.astype(np.int32)).view(torch.uint8).reshape(n, 20).cuda()
+
+
+def test_wildcard_grant_changes_decided_by_the_walk():
+    """A Watch batch that touches or deletes a document's wildcard grant keeps the label tables: the
+    document's slot is marked (kLjHdrWildDirty) rather than deferred, and its checks are decided in
+    the join from the slot without its wildcard entries, joined with a walk of the current rows for
+    the subject and for the wildcard (labels.inc lj_chain_wave, round 3). Bit-exact against the C
+    oracle after each of 16 batches, every check through the join, also for a subject that is dirty
+    itself."""
+    M = S.Mixed(0.05, device=torch.device("cuda", 0))
+    e, cav = load(M)
+    rng = np.random.default_rng(8)
+    n_docs = 0
+    for step in range(1, 17):
+        ups = M.churn(max(1, M.W.n_tuples // 100), cav)
+        e.apply_updates(1 + step, ups)
+        nd, items = _wild_checks(M, ups, rng)
+        if nd == 0:
+            continue
+        n_docs += nd
+        n = items.shape[0]
+        hi = items.cpu().numpy().view(corc.ITEM_DTYPE).reshape(-1)
+        e.reset_stats()
+        gp, ge = run(e, items)
+        st = e.stats()
+        cp, ce = M.expected(hi)
+        bad = np.nonzero((gp != cp) | (ge != ce))[0]
+        assert len(bad) == 0, (step, [(int(i), hi[i], int(gp[i]), int(cp[i])) for i in bad[:6]])
+        assert st["label_checks"] == n, (step, st["label_checks"], n)
+    assert n_docs >= 10, n_docs
+    e.close()
+
+
 def test_label_tables_hold_over_2000_batches():
     """The Watch stream of config 5 over 2,000 batches (0.1 % of the tuples each: at this scale
     every user's grants have changed several times, so nearly every subject is dirty and most
