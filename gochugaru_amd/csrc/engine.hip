@@ -2569,6 +2569,18 @@ static void aql_after_build(Engine& e) {
   }
 }
 
+// Has the last publication's null-stream work completed (no wait)? A batch submitted before it has
+// takes the HIP launch instead of the queue dispatch: its stream waits for that work on the device
+// (make_ctx), where aql_after_build would hold the host — config 5 submits its check batch right
+// after each Watch publication, and the host's spin on the merge cost its step 10-15 us.
+static bool aql_build_done(Engine& e) {
+  const uint64_t ps = e.patch_seq;
+  if (!ps || e.aql_patch_seen.load(std::memory_order_acquire) == ps) return true;
+  if (hipEventQuery((hipEvent_t)e.build_ev) != hipSuccess) return false;
+  e.aql_patch_seen.store(ps, std::memory_order_release);
+  return true;
+}
+
 static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uint32_t n, int64_t now_us,
                            uint8_t* d_perm, int32_t* d_err, hipStream_t st, bool host_out) {
   Ctx c = make_ctx(e, w, now_us, st, false);  // (the bundles below wait for the index patch: wait_patch)
@@ -2618,7 +2630,7 @@ static void bundles_launch(Engine& e, Workspace& w, const gck_item* d_items, uin
   // kernarg block and which clears the checks' caveat flags itself — nothing on the HIP stream)
   const bool aql_ok = w.b_own_stream && !host_out && !w.b_chained && ctr_was_clean && e.aql &&
                       w.aql_kernarg && (!w.cav_on || (lj && ds.lj_cav)) && (lj || cj) &&
-                      ((aql_timed && e.aql->tick_hz) || !w.b_timed);
+                      ((aql_timed && e.aql->tick_hz) || !w.b_timed) && aql_build_done(e);
   w.b_aql = false;
   w.b_res = false;
   w.b_sum_blocks = 0;

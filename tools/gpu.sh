@@ -107,6 +107,8 @@ case "$CMD" in
     timeout -k 10 300 python3 bench.py --no-cpu > "$OUT/bench_2000.json" 2> "$OUT/bench_2000.err"
     timeout -k 10 300 python3 bench.py --config mixed --steps 20 --warmup 5 > "$OUT/mixed20.json" 2> "$OUT/mixed20.err"
     timeout -k 10 400 python3 bench.py --config mixed --steps 500 --no-cpu > "$OUT/mixed500.json" 2> "$OUT/mixed500.err"
+    timeout -k 10 300 python3 bench.py --config gdocs --steps 20 --warmup 5 > "$OUT/gdocs20.json" 2> "$OUT/gdocs20.err"
+    timeout -k 10 400 python3 bench.py --config github --steps 20 --warmup 5 > "$OUT/github20.json" 2> "$OUT/github20.err"
     GCK_AQL_TIMED=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/kt.json" 2> "$OUT/kt.err"
     find "$OUT" -name "*kernel_trace.csv" -delete
