@@ -81,6 +81,19 @@ for step in "$@"; do
         || { tail -20 "$OUT/part_kt.err"; exit 1; }
       find "$OUT/part_kt" -name "*kernel_trace.csv" -delete
       find "$OUT/part_kt" -name "*agent_info.csv" -delete ;;
+    endbench)  # the round-end bench lines: the driver's default twice, 2,000 steps, configs 2 / 3 / 5
+      b driver1 300 --gpus 1 --steps 20 --warmup 5
+      b driver2 300 --gpus 1 --steps 20 --warmup 5
+      b bench2000 300 --no-cpu
+      b mixed20 300 --config mixed --steps 20 --warmup 5
+      b mixed500 400 --config mixed --steps 500 --no-cpu
+      b gdocs20 300 --config gdocs --steps 20 --warmup 5
+      b github20 400 --config github --steps 20 --warmup 5 ;;
+    endkt)
+      GCK_AQL_TIMED=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/kt.json" 2> "$OUT/kt.err" || { tail -20 "$OUT/kt.err"; exit 1; }
+      find "$OUT" -name "*kernel_trace.csv" -delete
+      find "$OUT" -name "*agent_info.csv" -delete ;;
     full)
       timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_full.log" 2>&1 || { tail -40 "$OUT/pytest_full.log"; exit 1; }
